@@ -1,0 +1,223 @@
+"""bench.py — batched BM25 CSC search throughput on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+      --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+A step = one search of the whole query batch (config c3: 1024 queries, k=100)
+over the 10M-doc / 200k-term / 640M-posting synthetic CSC index, inputs already
+resident in HBM.  With N GPUs the doc axis is sharded (one contiguous doc range
+per rank); every rank searches its shard, the per-shard
+[Q, k] lists are all-gathered over RCCL and merged on the GPU, so every step
+returns the same global top-k as one GPU would.  Total work is fixed as N
+grows ("scaling": "strong").
+
+Printed by rank 0: ONE JSON line with the metric, the roofline of the
+dominant kernel (score_tiles, timed with HIP events on its stream over the
+timed region) and the CPU baseline (the reference's scipy/numpy call
+sequence, oracle.search_faithful, on a bounded query sample, rank 0 at N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(REPO, "mojo-bm25_amd"), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(indptr: np.ndarray, queries: np.ndarray, k: int) -> int:
+    """B(q) = sum_{distinct t in q, t>=0} (8 df(t) + 8) + 4T + 8k."""
+    df = np.diff(indptr)
+    total = 0
+    for row in queries:
+        t = np.unique(row[row >= 0])
+        total += int((8 * df[t] + 8).sum()) + 4 * len(row) + 8 * k
+    return total
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def load_traffic(path: str, config: str, shift: int):
+    """HBM bytes per score_tiles launch measured offline with rocprofv3 --pmc
+    (profiles/) — used only if it matches this workload."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("config") == config and int(t.get("tile_shift", -1)) == shift:
+            return t.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--cpu-queries", type=int, default=-1,
+                    help="CPU baseline sample size (default: 16 for c3, 64 for c2; 0 = skip)")
+    ap.add_argument("--threads", type=int, default=16, help="host threads for index generation")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    from bm25mi import synth
+    from bm25mi.index import GpuIndex, merge_topk_device
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    cfg = synth.CONFIGS[args.config]
+    lo, hi = synth.shard_bounds(cfg.n_docs, world, rank)
+    t0 = time.time()
+    indptr, indices, data = synth.make_index(cfg, lo, hi, threads=args.threads)
+    log(f"[rank {rank}] shard docs [{lo},{hi}) nnz={int(indptr[-1])} generated in "
+        f"{time.time() - t0:.1f}s")
+    t0 = time.time()
+    index = GpuIndex(indptr, indices, data, hi - lo, device=local, doc_offset=lo)
+    info = index.info()
+    log(f"[rank {rank}] index on cuda:{local} in {time.time() - t0:.1f}s: {info}")
+    queries = synth.make_queries(cfg)
+    Q, T, k = queries.shape[0], queries.shape[1], cfg.k
+    dq = torch.from_numpy(queries).to(dev)
+    d_docs = torch.empty((Q, k), dtype=torch.int32, device=dev)
+    d_scores = torch.empty((Q, k), dtype=torch.float32, device=dev)
+    if world > 1:
+        g_docs = torch.empty((world, Q, k), dtype=torch.int32, device=dev)
+        g_scores = torch.empty((world, Q, k), dtype=torch.float32, device=dev)
+        m_docs = torch.empty((Q, k), dtype=torch.int32, device=dev)
+        m_scores = torch.empty((Q, k), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        index.search_device(dq, k, d_docs, d_scores, stream)
+        if world > 1:
+            dist.all_gather_into_tensor(g_docs, d_docs)
+            dist.all_gather_into_tensor(g_scores, d_scores)
+            merge_topk_device(local, g_docs, g_scores, world, Q, k, m_docs, m_scores, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    index.profile_enable(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    prof = index.profile_read()
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    qps = Q * args.steps / elapsed
+    # roofline of the dominant kernel on this rank (rank 0 reports its own)
+    alg_bytes = algorithmic_bytes(indptr, queries, k)
+    kern_ms = prof["score_ms"] / max(prof["score_launches"], 1)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    shift = int(np.log2(info["tile_docs"]))
+    traffic = load_traffic(args.traffic, args.config, shift) if world == 1 else None
+
+    cpu = None
+    if rank == 0 and world == 1:
+        nq = args.cpu_queries if args.cpu_queries >= 0 else (16 if args.config == "c3" else 64)
+        if nq > 0:
+            from oracle import oracle  # the checker / CPU baseline (test infrastructure)
+            sample = queries[:nq]
+            log(f"[rank 0] CPU baseline: bm25_native call sequence on {nq} queries ...")
+            t0 = time.perf_counter()
+            oracle.search_faithful(hi - lo, indptr, indices, data, sample, k)
+            dt = time.perf_counter() - t0
+            cpu = {"value": round(nq / dt, 3), "unit": "queries/s", "cores": 1, "kind": "port",
+                   "sample": f"first {nq} of the {Q} bench queries, same index, k={k}, "
+                             f"single process (scipy csc fancy-index + sum + argpartition, "
+                             f"bm25_native.py:149-158); {dt:.1f} s on {cpu_model()}, "
+                             f"host has {os.cpu_count()} logical cpus"}
+
+    if rank == 0:
+        out = {
+            "metric": "queries/sec + achieved HBM GB/s, 10M-doc CSC index, batch=1024, k=100"
+            if args.config == "c3" else f"queries/sec, {cfg.name}",
+            "value": round(qps, 2),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded Zipf CSC index + df^0.75 queries, csrc/synth.cpp)",
+            "config": {
+                "workload": f"{args.config}: {cfg.name}",
+                "n_docs": cfg.n_docs, "n_terms": cfg.n_terms, "nnz": int(indptr[-1]) if world == 1
+                else cfg.nnz, "batch": Q, "terms_per_query": T, "k": k,
+                "tile_docs": info["tile_docs"],
+                "parallelism": f"doc-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic,
+                "kernel": "score_tiles",
+                "kernel_ms": round(kern_ms, 4),
+                "alg_bytes_per_launch": alg_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    index.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

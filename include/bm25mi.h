@@ -1,0 +1,144 @@
+/*
+ * bm25mi.h — C-ABI of libbm25mi.so, the MI355X-native BM25 CSC query engine.
+ *
+ * This is the drop-in boundary for the reference's batched BM25 scoring path
+ * (SURVEY.md §8(b)).  Every entry point is plain C: pointers, sizes and error
+ * codes, no torch / HIP types in the signatures.  Each function cites the
+ * reference interface it replaces (paths relative to the reference checkout
+ * yuhuishi-convect/mojo-bm25 @ 2025-06-20).
+ *
+ * Conventions
+ *   - Return 0 on success, a BM25_E* code otherwise; the message of the last
+ *     failure on the calling thread is bm25_last_error().
+ *   - Host buffers are C-order numpy-compatible arrays owned by the caller.
+ *   - Device buffers (the *_device entry points) are caller-owned HIP device
+ *     allocations on the index's device; `stream` is a hipStream_t passed as
+ *     void* (NULL = the legacy default stream).  *_device calls are
+ *     asynchronous with respect to the host.
+ *   - One index handle is not re-entrant: calls on the same handle are
+ *     serialised by an internal mutex.
+ *   - Doc ids are int32, scores float32, token ids int32; negative token ids
+ *     are padding and are skipped (bm25_native.py:151).
+ *   - Results are sorted by score descending; equal scores are ordered by doc
+ *     id ascending (the deterministic rule of the MAX CPU top-k,
+ *     operations/topk.mojo:234-258 / test_topk.mojo:222-238; bm25_native's
+ *     own tie order is numpy-implementation-defined).
+ */
+#ifndef BM25MI_H
+#define BM25MI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BM25MI_ABI_VERSION 1
+
+enum {
+  BM25_OK = 0,
+  BM25_EINVAL = 1, /* bad argument (bad shape, token id >= n_terms, k > n_docs ...) */
+  BM25_EHIP = 2,   /* HIP runtime failure, or no usable GPU */
+  BM25_ERCCL = 3,  /* RCCL failure (sharded handles) */
+  BM25_ENOMEM = 4  /* device or host allocation failed */
+};
+
+typedef struct bm25_index bm25_index;
+
+/* ABI version of the loaded library (== BM25MI_ABI_VERSION it was built with). */
+int bm25_abi_version(void);
+
+/* Message of the last failing call on this thread ("" if none).  The pointer
+ * stays valid until the next failing call on the same thread. */
+const char* bm25_last_error(void);
+
+/* Number of HIP devices visible to the process (0 on a host without a GPU;
+ * never fails). */
+int bm25_device_count(void);
+
+/*
+ * Build a device-resident index from a CSC doc x term score matrix.
+ * Replaces: BM25v.index(doc_toks: scipy csc_matrix, doc_lengths)
+ *           (bm25_native.py:59-74) and the host->device copy of the MAX path
+ *           (gpu_bm25/common.py:38).
+ *   indptr  [n_terms+1]  int32 (indptr_is_i64 = 0) or int64 (= 1), indptr[0]=0,
+ *                        indptr[n_terms] = nnz, non-decreasing
+ *   indices [nnz] int32  doc ids of each column, sorted ascending and unique
+ *                        within a column (canonical CSC, as bm25s writes it)
+ *   data    [nnz] f32    precomputed per-(doc, term) BM25 scores
+ * The arrays are copied; the caller may free them when this returns.
+ * doc_offset is added to every doc id the index returns (shards of a larger
+ * collection pass the global id of their first document; 0 otherwise).
+ */
+int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
+                      const void* indptr, int indptr_is_i64,
+                      const int32_t* indices, const float* data,
+                      int64_t doc_offset, bm25_index** out);
+
+/* Release every device allocation and stream of the handle. */
+int bm25_index_destroy(bm25_index* idx);
+
+/* Geometry of a built index (any pointer may be NULL). */
+int bm25_index_info(const bm25_index* idx, int64_t* n_docs, int64_t* n_terms,
+                    int64_t* nnz, int32_t* tile_docs, int64_t* n_tiles,
+                    int64_t* device_bytes);
+
+/*
+ * Batched top-k search, host buffers, synchronous.
+ * Replaces: BM25v.search / get_scores / _compute_relevance_from_scores / _topk
+ *           (bm25_native.py:76-158, 204-214).
+ *   queries    [Q, T] int32, negative = padding, every id < n_terms
+ *   out_docs   [Q, k] int32
+ *   out_scores [Q, k] f32
+ * Errors: EINVAL when a token id >= n_terms (message matches
+ * bm25_native.py:118-121), when k < 0 or k > n_docs.
+ */
+int bm25_search(bm25_index* idx, const int32_t* queries, int64_t Q, int64_t T,
+                int32_t k, int32_t* out_docs, float* out_scores);
+
+/*
+ * Same as bm25_search with device-resident queries and results, enqueued on
+ * `stream` without host synchronisation (the bench's timed step: inputs
+ * already resident in HBM).  Token ids are NOT validated on the host here:
+ * ids >= n_terms are treated as padding by the kernels.
+ */
+int bm25_search_device(bm25_index* idx, const int32_t* d_queries, int64_t Q,
+                       int64_t T, int32_t k, int32_t* d_docs, float* d_scores,
+                       void* stream);
+
+/*
+ * Dense per-document scores of one query (all n_docs fp32 sums, query-term
+ * order, zero for untouched documents), host buffers.
+ * Replaces: the dense gather+sum of the MAX graph (gpu_bm25/common.py:64-74)
+ *           and BM25.get_scores (bm25.py:124-145) over a CSC index.
+ */
+int bm25_scores_dense(bm25_index* idx, const int32_t* query, int64_t T,
+                      float* out_scores);
+
+/*
+ * Merge W per-shard top-k lists (global doc ids) into one top-k, device
+ * buffers: d_docs/d_scores are [W, Q, k], outputs [Q, k].  Used after the
+ * RCCL all-gather of the doc-sharded search; the order rule
+ * is the same (score desc, doc asc), so the result equals a single-index
+ * search over the whole collection.
+ */
+int bm25_merge_topk_device(int device, const int32_t* d_docs,
+                           const float* d_scores, int64_t W, int64_t Q,
+                           int32_t k, int32_t* d_out_docs, float* d_out_scores,
+                           void* stream);
+
+/*
+ * Kernel timing of the dominant kernel (score_tiles), measured with HIP
+ * events recorded on the search stream around every launch while enabled.
+ * bm25_profile_enable(idx, 1) resets the accumulators.
+ */
+int bm25_profile_enable(bm25_index* idx, int on);
+int bm25_profile_read(bm25_index* idx, double* score_ms_total,
+                      int64_t* score_launches, double* total_ms,
+                      int64_t* searches, int64_t* rescored_tiles);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BM25MI_H */

@@ -1,0 +1,55 @@
+"""Build the in-tree shared libraries (no JIT cache: the .so files travel with
+the repo snapshot to the GPU box).
+
+  libbm25mi.so     hipcc --offload-arch=gfx950: kernels + C-ABI (the product)
+  libbm25synth.so  g++: synthetic index / query generator (bench + tests data)
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(PKG_DIR), "csrc")
+REPO = os.path.dirname(os.path.dirname(PKG_DIR))
+LIB = os.path.join(PKG_DIR, "libbm25mi.so")
+SYNTH_LIB = os.path.join(PKG_DIR, "libbm25synth.so")
+
+HIP_SOURCES = ["bm25mi_kernels.hip", "bm25mi_capi.cpp"]
+HIP_DEPS = HIP_SOURCES + ["bm25mi_internal.h"]
+ARCH = os.environ.get("BM25_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build(force: bool = False, verbose: bool = False) -> None:
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    deps = [os.path.join(CSRC, s) for s in HIP_DEPS] + [os.path.join(REPO, "include", "bm25mi.h")]
+    if force or _stale(LIB, deps):
+        tmp = LIB + ".tmp"
+        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-Wno-unused-result", "-Wno-unused-value", "-o", tmp]
+             + [os.path.join(CSRC, s) for s in HIP_SOURCES], verbose)
+        os.replace(tmp, LIB)
+    sdeps = [os.path.join(CSRC, "synth.cpp")]
+    if force or _stale(SYNTH_LIB, sdeps):
+        tmp = SYNTH_LIB + ".tmp"
+        _run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-fPIC", "-shared", "-pthread",
+              "-o", tmp, sdeps[0]], verbose)
+        os.replace(tmp, SYNTH_LIB)
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,149 @@
+"""GpuIndex — a device-resident BM25 CSC index on one MI355X.
+
+Host mirror of the reference's index object (bm25_native.BM25v.doc_toks,
+bm25_native.py:59-74) backed by libbm25mi.so.  All compute goes through the
+C-ABI; this module only validates, converts dtypes and owns the handle.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class GpuIndex:
+    """A doc x term CSC score matrix resident in HBM.
+
+    Arguments mirror ``scipy.sparse.csc_matrix((data, indices, indptr),
+    shape=(n_docs, n_terms))`` — the in-memory form of the bm25s on-disk
+    index (indptr/indices/data ``.csc.index.npy``)."""
+
+    def __init__(self, indptr, indices, data, n_docs: int, device: int = 0,
+                 doc_offset: int = 0):
+        indptr = np.asarray(indptr)
+        if indptr.ndim != 1 or indptr.size < 1:
+            raise ValueError("indptr must be a 1-D array of n_terms + 1 offsets")
+        ip_i64 = indptr.dtype == np.int64 or indptr[-1] > np.iinfo(np.int32).max
+        self._indptr = np.ascontiguousarray(indptr, dtype=np.int64 if ip_i64 else np.int32)
+        self._indices = np.ascontiguousarray(indices, dtype=np.int32)
+        self._data = np.ascontiguousarray(data, dtype=np.float32)
+        nnz = int(self._indptr[-1])
+        if self._indices.size < nnz or self._data.size < nnz:
+            raise ValueError("indices/data shorter than indptr[-1]")
+        self.n_docs = int(n_docs)
+        self.n_terms = int(self._indptr.size - 1)
+        self.nnz = nnz
+        self.device = int(device)
+        self.doc_offset = int(doc_offset)
+        h = ctypes.c_void_p()
+        self._h = None
+        check(lib.bm25_index_create(self.device, self.n_docs, self.n_terms, nnz,
+                                    _ptr(self._indptr), int(ip_i64), _ptr(self._indices),
+                                    _ptr(self._data), self.doc_offset, ctypes.byref(h)))
+        self._h = h
+        # the device holds its own copy
+        self._indptr = self._indices = self._data = None
+
+    # ------------------------------------------------------------------
+    @classmethod
+    def from_csc(cls, m, device: int = 0, doc_offset: int = 0) -> "GpuIndex":
+        """From a scipy.sparse CSC matrix (doc x term).  Non-canonical input
+        (unsorted indices) is sorted on a copy first; duplicate entries are
+        summed (scipy semantics for a CSC with duplicates)."""
+        import scipy.sparse as sp
+        if not sp.issparse(m):
+            raise ValueError("doc_toks must be a scipy.sparse matrix")
+        m = m.tocsc()
+        if not m.has_canonical_format:
+            m = m.copy()
+            m.sum_duplicates()
+        return cls(m.indptr, m.indices, m.data, m.shape[0], device=device, doc_offset=doc_offset)
+
+    # ------------------------------------------------------------------
+    def close(self) -> None:
+        if self._h is not None:
+            lib.bm25_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        vals = [ctypes.c_int64() for _ in range(3)]
+        td = ctypes.c_int32()
+        nt = ctypes.c_int64()
+        db = ctypes.c_int64()
+        check(lib.bm25_index_info(self._h, *[ctypes.byref(v) for v in vals], ctypes.byref(td),
+                                  ctypes.byref(nt), ctypes.byref(db)))
+        return {"n_docs": vals[0].value, "n_terms": vals[1].value, "nnz": vals[2].value,
+                "tile_docs": td.value, "n_tiles": nt.value, "device_bytes": db.value}
+
+    # ------------------------------------------------------------------
+    def search(self, queries: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        """Top-k of every query row (host arrays).  queries: int32 [Q, T]."""
+        q = np.ascontiguousarray(queries, dtype=np.int32)
+        if q.ndim != 2:
+            raise ValueError("queries must be a 2-D [Q, T] int32 array")
+        Q, T = q.shape
+        k = int(k)
+        docs = np.zeros((Q, max(k, 0)), np.int32)
+        scores = np.zeros((Q, max(k, 0)), np.float32)
+        check(lib.bm25_search(self._h, _ptr(q), Q, T, k, _ptr(docs), _ptr(scores)))
+        return docs, scores
+
+    def search_device(self, d_queries, k: int, d_docs, d_scores, stream=None) -> None:
+        """Device-resident search: torch int32 [Q, T] in, int32/f32 [Q, k] out,
+        enqueued on ``stream`` (a torch.cuda.Stream or raw handle)."""
+        Q, T = d_queries.shape
+        s = getattr(stream, "cuda_stream", stream) or 0
+        check(lib.bm25_search_device(self._h, ctypes.c_void_p(d_queries.data_ptr()), Q, T,
+                                     int(k), ctypes.c_void_p(d_docs.data_ptr()),
+                                     ctypes.c_void_p(d_scores.data_ptr()), ctypes.c_void_p(s)))
+
+    def scores_dense(self, query) -> np.ndarray:
+        """All n_docs fp32 scores of one query (zero for untouched docs)."""
+        q = np.ascontiguousarray(np.asarray(query).ravel(), dtype=np.int32)
+        out = np.zeros(self.n_docs, np.float32)
+        check(lib.bm25_scores_dense(self._h, _ptr(q), q.size, _ptr(out)))
+        return out
+
+    # ------------------------------------------------------------------
+    def profile_enable(self, on: bool = True) -> None:
+        check(lib.bm25_profile_enable(self._h, int(on)))
+
+    def profile_read(self) -> dict:
+        sm = ctypes.c_double()
+        sl = ctypes.c_int64()
+        tm = ctypes.c_double()
+        ns = ctypes.c_int64()
+        rs = ctypes.c_int64()
+        check(lib.bm25_profile_read(self._h, ctypes.byref(sm), ctypes.byref(sl), ctypes.byref(tm),
+                                    ctypes.byref(ns), ctypes.byref(rs)))
+        return {"score_ms": sm.value, "score_launches": sl.value, "total_ms": tm.value,
+                "searches": ns.value, "rescored_tiles_last": rs.value}
+
+
+def merge_topk_device(device: int, d_docs, d_scores, W: int, Q: int, k: int, d_out_docs,
+                      d_out_scores, stream=None) -> None:
+    """Merge W per-shard [Q, k] lists (global doc ids) -> [Q, k] on the GPU."""
+    s = getattr(stream, "cuda_stream", stream) or 0
+    check(lib.bm25_merge_topk_device(int(device), ctypes.c_void_p(d_docs.data_ptr()),
+                                     ctypes.c_void_p(d_scores.data_ptr()), int(W), int(Q), int(k),
+                                     ctypes.c_void_p(d_out_docs.data_ptr()),
+                                     ctypes.c_void_p(d_out_scores.data_ptr()),
+                                     ctypes.c_void_p(s)))
+
+
+def device_count() -> int:
+    return _capi.device_count()

@@ -1,0 +1,433 @@
+// bm25mi_capi.cpp — the extern "C" boundary of libbm25mi.so (include/bm25mi.h).
+//
+// Host side of the drop-in: validation with the reference's error behaviour
+// (bm25_native.py:105-127), index upload + device layout build, workspace
+// management and the search pipeline (score_tiles -> merge -> rescore ->
+// merge_final), all on one HIP stream per handle.
+#include "../../include/bm25mi.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bm25mi_internal.h"
+
+using namespace bm25mi;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? BM25_ENOMEM : BM25_EHIP, "%s: %s (%s)", what,
+              hipGetErrorString(e), hipGetErrorName(e));
+}
+
+#define HIP_TRY(expr, what)                 \
+  do {                                      \
+    hipError_t e_ = (expr);                 \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+struct EventPair {
+  hipEvent_t a = nullptr, b = nullptr, c = nullptr;  // start, after score pass, end
+};
+
+}  // namespace
+
+struct bm25_index {
+  DevIndex ix;
+  hipStream_t stream = nullptr;
+  Workspace ws;
+  // host-call staging buffers (device)
+  int32_t* d_q = nullptr;
+  int32_t* d_docs = nullptr;
+  float* d_scores = nullptr;
+  int64_t cap_q_elems = 0, cap_out_elems = 0;
+  std::mutex mu;
+  // profiling
+  bool prof = false;
+  std::vector<EventPair> ev_pool;
+  size_t ev_used = 0;
+  double score_ms = 0.0, total_ms = 0.0;
+  int64_t score_launches = 0, searches = 0, rescored = 0;
+  int64_t device_bytes = 0;
+};
+
+namespace {
+
+void free_ws(Workspace& ws) {
+  hipFree(ws.cand);
+  hipFree(ws.cand2);
+  hipFree(ws.flag_tiles);
+  hipFree(ws.nflag);
+  hipFree(ws.counters);
+  hipFree(ws.queue);
+  ws = Workspace{};
+}
+
+int ensure_ws(bm25_index* h, int64_t Q, int k) {
+  Workspace& ws = h->ws;
+  if (Q <= ws.cap_q && k <= ws.cap_k) return BM25_OK;
+  const int64_t q = std::max(Q, ws.cap_q);
+  const int64_t kk = std::max<int64_t>(k, ws.cap_k);
+  free_ws(ws);
+  const int64_t mf = maxflag_for((int)kk, h->ix.ntiles);
+  HIP_TRY(hipMalloc(&ws.cand, sizeof(uint64_t) * q * h->ix.ntiles * kTileM), "hipMalloc(cand)");
+  HIP_TRY(hipMalloc(&ws.cand2, sizeof(uint64_t) * q * mf * kk), "hipMalloc(cand2)");
+  HIP_TRY(hipMalloc(&ws.flag_tiles, sizeof(int32_t) * q * mf), "hipMalloc(flag_tiles)");
+  HIP_TRY(hipMalloc(&ws.nflag, sizeof(int32_t) * q), "hipMalloc(nflag)");
+  HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
+  HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
+  ws.cap_q = q;
+  ws.cap_k = kk;
+  return BM25_OK;
+}
+
+int ensure_io(bm25_index* h, int64_t q_elems, int64_t out_elems) {
+  if (q_elems > h->cap_q_elems) {
+    hipFree(h->d_q);
+    h->d_q = nullptr;
+    HIP_TRY(hipMalloc(&h->d_q, sizeof(int32_t) * std::max<int64_t>(q_elems, 1)), "hipMalloc(queries)");
+    h->cap_q_elems = q_elems;
+  }
+  if (out_elems > h->cap_out_elems) {
+    hipFree(h->d_docs);
+    hipFree(h->d_scores);
+    h->d_docs = nullptr;
+    h->d_scores = nullptr;
+    HIP_TRY(hipMalloc(&h->d_docs, sizeof(int32_t) * std::max<int64_t>(out_elems, 1)), "hipMalloc(docs)");
+    HIP_TRY(hipMalloc(&h->d_scores, sizeof(float) * std::max<int64_t>(out_elems, 1)), "hipMalloc(scores)");
+    h->cap_out_elems = out_elems;
+  }
+  return BM25_OK;
+}
+
+void harvest_events(bm25_index* h) {
+  if (h->ev_used == 0) return;
+  for (size_t i = 0; i < h->ev_used; ++i) {
+    float ms1 = 0.f, ms2 = 0.f;
+    hipEventSynchronize(h->ev_pool[i].c);  // events may sit on a caller's stream
+    hipEventElapsedTime(&ms1, h->ev_pool[i].a, h->ev_pool[i].b);
+    hipEventElapsedTime(&ms2, h->ev_pool[i].a, h->ev_pool[i].c);
+    h->score_ms += ms1;
+    h->total_ms += ms2;
+  }
+  h->ev_used = 0;
+}
+
+EventPair* next_events(bm25_index* h) {
+  if (!h->prof) return nullptr;
+  if (h->ev_used == h->ev_pool.size()) {
+    if (h->ev_pool.size() < 512) {
+      EventPair p;
+      hipEventCreate(&p.a);
+      hipEventCreate(&p.b);
+      hipEventCreate(&p.c);
+      h->ev_pool.push_back(p);
+    } else {
+      harvest_events(h);
+    }
+  }
+  return &h->ev_pool[h->ev_used++];
+}
+
+// Device pipeline on stream st; caller holds h->mu and has set the device.
+int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, int k,
+               int32_t* d_docs, float* d_scores, hipStream_t st) {
+  if (Q == 0 || k == 0) return BM25_OK;
+  int rc = ensure_ws(h, Q, k);
+  if (rc) return rc;
+  EventPair* ev = next_events(h);
+  if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
+  HIP_TRY(launch_score_tiles(h->ix, d_queries, Q, T, h->ws, st), "score_tiles launch");
+  if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
+  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, h->ws, d_docs, d_scores, st), "select launch");
+  if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
+  if (h->prof) {
+    h->score_launches += 1;
+    h->searches += 1;
+  }
+  return BM25_OK;
+}
+
+int check_k(const bm25_index* h, int64_t k) {
+  if (k < 0) return fail(BM25_EINVAL, "negative dimensions are not allowed (top_k=%lld)", (long long)k);
+  if (k > h->ix.n_docs)
+    return fail(BM25_EINVAL, "kth(=%lld) out of bounds (%lld)", (long long)(h->ix.n_docs - k),
+                (long long)h->ix.n_docs);
+  if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%lld exceeds the engine limit %d", (long long)k, kMaxK);
+  return BM25_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bm25_abi_version(void) { return BM25MI_ABI_VERSION; }
+
+const char* bm25_last_error(void) { return g_err.c_str(); }
+
+int bm25_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
+                      const void* indptr, int indptr_is_i64, const int32_t* indices,
+                      const float* data, int64_t doc_offset, bm25_index** out) {
+  if (!out) return fail(BM25_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (n_docs < 0 || n_terms < 0 || nnz < 0)
+    return fail(BM25_EINVAL, "negative size (n_docs=%lld n_terms=%lld nnz=%lld)",
+                (long long)n_docs, (long long)n_terms, (long long)nnz);
+  if (n_docs > INT32_MAX) return fail(BM25_EINVAL, "n_docs=%lld exceeds int32 doc ids", (long long)n_docs);
+  if (doc_offset < 0 || doc_offset + n_docs > (int64_t)INT32_MAX + 1)
+    return fail(BM25_EINVAL, "doc_offset=%lld out of int32 range", (long long)doc_offset);
+  if (!indptr || (nnz > 0 && (!indices || !data)))
+    return fail(BM25_EINVAL, "NULL CSC array");
+  // indptr on the host: int64, validated O(V)
+  std::vector<int64_t> ip(n_terms + 1);
+  for (int64_t t = 0; t <= n_terms; ++t)
+    ip[t] = indptr_is_i64 ? ((const int64_t*)indptr)[t] : (int64_t)((const int32_t*)indptr)[t];
+  if (ip[0] != 0 || ip[n_terms] != nnz)
+    return fail(BM25_EINVAL, "indptr must start at 0 and end at nnz (got %lld..%lld, nnz=%lld)",
+                (long long)ip[0], (long long)ip[n_terms], (long long)nnz);
+  for (int64_t t = 0; t < n_terms; ++t) {
+    if (ip[t + 1] < ip[t]) return fail(BM25_EINVAL, "indptr decreases at column %lld", (long long)t);
+    if (ip[t + 1] - ip[t] > n_docs)
+      return fail(BM25_EINVAL, "column %lld has more entries than n_docs", (long long)t);
+  }
+  int shift = env_int("BM25_TILE_SHIFT", 14);
+  if (!tile_shift_supported(shift)) return fail(BM25_EINVAL, "BM25_TILE_SHIFT=%d not compiled (13,14,15)", shift);
+  const int64_t ntiles = (n_docs + (1LL << shift) - 1) >> shift;
+  if (ntiles > 65536) return fail(BM25_EINVAL, "n_docs=%lld needs %lld tiles (> 65536)", (long long)n_docs, (long long)ntiles);
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(BM25_EHIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(BM25_EINVAL, "device %d out of range (%d visible)", device, ndev);
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+
+  bm25_index* h = new bm25_index();
+  DevIndex& ix = h->ix;
+  ix.device = device;
+  ix.n_docs = n_docs;
+  ix.n_terms = n_terms;
+  ix.nnz = nnz;
+  ix.doc_offset = doc_offset;
+  ix.tile_shift = shift;
+  ix.ntiles = ntiles;
+  int32_t* d_indices = nullptr;
+  int32_t* d_err = nullptr;
+  auto cleanup = [&](int rc) {
+    hipFree(d_indices);
+    hipFree(d_err);
+    if (rc != BM25_OK) bm25_index_destroy(h);
+    return rc;
+  };
+  hipError_t e;
+#define TRYC(expr, what)                                          \
+  do {                                                            \
+    e = (expr);                                                   \
+    if (e != hipSuccess) return cleanup(hip_fail(e, what));       \
+  } while (0)
+  TRYC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+  const int64_t rel_elems = n_terms * (ntiles + 1);
+  TRYC(hipMalloc(&ix.indptr, sizeof(int64_t) * (n_terms + 1)), "hipMalloc(indptr)");
+  TRYC(hipMalloc(&ix.rel, sizeof(uint32_t) * std::max<int64_t>(rel_elems, 1)), "hipMalloc(rel)");
+  TRYC(hipMalloc(&ix.ldoc, sizeof(uint16_t) * std::max<int64_t>(nnz, 1)), "hipMalloc(ldoc)");
+  TRYC(hipMalloc(&ix.val, sizeof(float) * std::max<int64_t>(nnz, 1)), "hipMalloc(val)");
+  TRYC(hipMalloc(&d_indices, sizeof(int32_t) * std::max<int64_t>(nnz, 1)), "hipMalloc(indices)");
+  TRYC(hipMalloc(&d_err, sizeof(int32_t)), "hipMalloc(err)");
+  h->device_bytes = (int64_t)(sizeof(int64_t) * (n_terms + 1) + sizeof(uint32_t) * rel_elems +
+                              (sizeof(uint16_t) + sizeof(float)) * nnz);
+  TRYC(hipMemsetAsync(d_err, 0, sizeof(int32_t), h->stream), "hipMemset");
+  TRYC(hipMemcpyAsync(ix.indptr, ip.data(), sizeof(int64_t) * (n_terms + 1), hipMemcpyHostToDevice, h->stream), "H2D indptr");
+  if (nnz > 0) {
+    TRYC(hipMemcpyAsync(d_indices, indices, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, h->stream), "H2D indices");
+    TRYC(hipMemcpyAsync(ix.val, data, sizeof(float) * nnz, hipMemcpyHostToDevice, h->stream), "H2D data");
+  }
+  TRYC(launch_build_tables(ix, d_indices, d_err, h->stream), "build_tables launch");
+  int32_t herr = 0;
+  TRYC(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), "D2H err");
+  TRYC(hipStreamSynchronize(h->stream), "build sync");
+#undef TRYC
+  if (herr)
+    return cleanup(fail(BM25_EINVAL,
+                        "indices must be sorted, unique and in [0, n_docs) within every column "
+                        "(canonical CSC)"));
+  *out = h;
+  return cleanup(BM25_OK);
+}
+
+int bm25_index_destroy(bm25_index* h) {
+  if (!h) return BM25_OK;
+  hipSetDevice(h->ix.device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  for (auto& p : h->ev_pool) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+    hipEventDestroy(p.c);
+  }
+  free_ws(h->ws);
+  hipFree(h->d_q);
+  hipFree(h->d_docs);
+  hipFree(h->d_scores);
+  hipFree(h->ix.indptr);
+  hipFree(h->ix.rel);
+  hipFree(h->ix.ldoc);
+  hipFree(h->ix.val);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return BM25_OK;
+}
+
+int bm25_index_info(const bm25_index* h, int64_t* n_docs, int64_t* n_terms, int64_t* nnz,
+                    int32_t* tile_docs, int64_t* n_tiles, int64_t* device_bytes) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (n_docs) *n_docs = h->ix.n_docs;
+  if (n_terms) *n_terms = h->ix.n_terms;
+  if (nnz) *nnz = h->ix.nnz;
+  if (tile_docs) *tile_docs = 1 << h->ix.tile_shift;
+  if (n_tiles) *n_tiles = h->ix.ntiles;
+  if (device_bytes) *device_bytes = h->device_bytes;
+  return BM25_OK;
+}
+
+int bm25_search(bm25_index* h, const int32_t* queries, int64_t Q, int64_t T, int32_t k,
+                int32_t* out_docs, float* out_scores) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (Q < 0 || T < 0) return fail(BM25_EINVAL, "negative query shape");
+  int rc = check_k(h, k);
+  if (rc) return rc;
+  if (Q == 0 || k == 0) return BM25_OK;
+  if (T > 0 && !queries) return fail(BM25_EINVAL, "NULL queries");
+  if (!out_docs || !out_scores) return fail(BM25_EINVAL, "NULL output");
+  // bm25_native.py:116-121: max(initial=0) >= n_terms -> ValueError
+  int64_t mx = 0;
+  for (int64_t i = 0; i < Q * T; ++i) mx = std::max<int64_t>(mx, queries[i]);
+  if (mx >= h->ix.n_terms)
+    return fail(BM25_EINVAL,
+                "The maximum token ID in the query (%lld) is higher than the number of tokens in "
+                "the index.",
+                (long long)mx);
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  rc = ensure_io(h, Q * T, Q * (int64_t)k);
+  if (rc) return rc;
+  if (Q * T > 0)
+    HIP_TRY(hipMemcpyAsync(h->d_q, queries, sizeof(int32_t) * Q * T, hipMemcpyHostToDevice, h->stream), "H2D queries");
+  rc = run_search(h, h->d_q, Q, T, k, h->d_docs, h->d_scores, h->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_docs, h->d_docs, sizeof(int32_t) * Q * k, hipMemcpyDeviceToHost, h->stream), "D2H docs");
+  HIP_TRY(hipMemcpyAsync(out_scores, h->d_scores, sizeof(float) * Q * k, hipMemcpyDeviceToHost, h->stream), "D2H scores");
+  HIP_TRY(hipStreamSynchronize(h->stream), "search sync");
+  return BM25_OK;
+}
+
+int bm25_search_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, int32_t k,
+                       int32_t* d_docs, float* d_scores, void* stream) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (Q < 0 || T < 0) return fail(BM25_EINVAL, "negative query shape");
+  int rc = check_k(h, k);
+  if (rc) return rc;
+  if (Q == 0 || k == 0) return BM25_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  return run_search(h, d_queries, Q, T, k, d_docs, d_scores, (hipStream_t)stream);
+}
+
+int bm25_scores_dense(bm25_index* h, const int32_t* query, int64_t T, float* out_scores) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (T < 0) return fail(BM25_EINVAL, "negative query length");
+  if (!out_scores) return fail(BM25_EINVAL, "NULL output");
+  int64_t mx = 0;
+  for (int64_t i = 0; i < T; ++i) mx = std::max<int64_t>(mx, query[i]);
+  if (mx >= h->ix.n_terms)
+    return fail(BM25_EINVAL,
+                "The maximum token ID in the query (%lld) is higher than the number of tokens in "
+                "the index.",
+                (long long)mx);
+  if (h->ix.n_docs == 0) return BM25_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  float* d_out = nullptr;
+  int32_t* d_qq = nullptr;
+  HIP_TRY(hipMalloc(&d_out, sizeof(float) * h->ix.n_docs), "hipMalloc(dense)");
+  hipError_t e = hipMalloc(&d_qq, sizeof(int32_t) * std::max<int64_t>(T, 1));
+  if (e == hipSuccess && T > 0)
+    e = hipMemcpyAsync(d_qq, query, sizeof(int32_t) * T, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = launch_scores_dense(h->ix, d_qq, T, d_out, h->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(out_scores, d_out, sizeof(float) * h->ix.n_docs, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  hipFree(d_out);
+  hipFree(d_qq);
+  if (e != hipSuccess) return hip_fail(e, "scores_dense");
+  return BM25_OK;
+}
+
+int bm25_merge_topk_device(int device, const int32_t* d_docs, const float* d_scores, int64_t W,
+                           int64_t Q, int32_t k, int32_t* d_out_docs, float* d_out_scores,
+                           void* stream) {
+  if (W < 1 || Q < 0 || k < 0) return fail(BM25_EINVAL, "bad merge shape W=%lld Q=%lld k=%d", (long long)W, (long long)Q, k);
+  if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%d exceeds the engine limit %d", k, kMaxK);
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+  HIP_TRY(launch_merge_lists(d_docs, d_scores, W, Q, k, d_out_docs, d_out_scores, (hipStream_t)stream), "merge_lists launch");
+  return BM25_OK;
+}
+
+int bm25_profile_enable(bm25_index* h, int on) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  std::lock_guard<std::mutex> lk(h->mu);
+  hipSetDevice(h->ix.device);
+  harvest_events(h);
+  h->prof = on != 0;
+  h->score_ms = h->total_ms = 0.0;
+  h->score_launches = h->searches = h->rescored = 0;
+  return BM25_OK;
+}
+
+int bm25_profile_read(bm25_index* h, double* score_ms_total, int64_t* score_launches,
+                      double* total_ms, int64_t* searches, int64_t* rescored_tiles) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  std::lock_guard<std::mutex> lk(h->mu);
+  hipSetDevice(h->ix.device);
+  harvest_events(h);
+  int32_t cnt[4] = {0, 0, 0, 0};
+  if (h->ws.counters) {
+    hipMemcpyAsync(cnt, h->ws.counters, sizeof cnt, hipMemcpyDeviceToHost, h->stream);
+    hipStreamSynchronize(h->stream);
+  }
+  if (score_ms_total) *score_ms_total = h->score_ms;
+  if (score_launches) *score_launches = h->score_launches;
+  if (total_ms) *total_ms = h->total_ms;
+  if (searches) *searches = h->searches;
+  if (rescored_tiles) *rescored_tiles = cnt[0];  // items queued by the last search
+  return BM25_OK;
+}
+
+}  // extern "C"

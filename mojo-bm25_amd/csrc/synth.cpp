@@ -1,0 +1,220 @@
+// synth.cpp — seeded synthetic CSC BM25 indices and query batches
+// (libbm25synth.so, host only).  This is the data source of bench.py and of
+// the large parity tests: the reference ships no large index, so the configs
+// of BASELINE.md are generated here, deterministically and shard-independently.
+//
+// Model (BASELINE.md §3 / SURVEY.md §8(d)):
+//   df_target(t) = clamp(round(C / (t+1)^alpha), 1, N/2), C solved so that
+//                  sum_t df_target(t) ~= nnz_target   (term 0 most frequent)
+//   postings     docs of term t are a Bernoulli(p_t = df_target/N) process,
+//                sampled by geometric gaps inside 16384-doc chunks, each
+//                (term, chunk) with its own splitmix64 stream, so any doc
+//                range (a shard) can be generated alone and agrees with the
+//                full index; ids are sorted and unique per column
+//   data         idf(t) * u, u ~ U(0.1, 1.0) in f32, with the lucene idf
+//                ln(1 + (N - df + 0.5) / (df + 0.5)) of df_target
+//   queries      T distinct terms per query, drawn with probability
+//                proportional to df_target^beta (beta = 0.75)
+#include <stdint.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <thread>
+#include <vector>
+
+namespace {
+
+constexpr int64_t kChunk = 16384;
+
+inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct Rng {
+  uint64_t s;
+  explicit Rng(uint64_t seed) : s(seed) {}
+  uint64_t next() {
+    s += 0x9E3779B97F4A7C15ull;
+    return mix64(s);
+  }
+  // uniform in (0, 1]
+  double unit() { return ((double)(next() >> 11) + 1.0) * (1.0 / 9007199254740992.0); }
+};
+
+uint64_t stream_seed(uint64_t seed, int64_t a, int64_t b) {
+  uint64_t h = mix64(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(a + 1));
+  return mix64(h ^ (0xD1B54A32D192ED03ull * (uint64_t)(b + 1)));
+}
+
+struct Plan {
+  int64_t N, V;
+  std::vector<int64_t> df;
+  std::vector<double> inv_log1m;  // 1 / log(1 - p), 0 when p >= 1
+  std::vector<float> idf;
+  std::vector<uint8_t> all;       // p >= 1: every doc
+};
+
+void solve_df(int64_t N, int64_t V, int64_t nnz, double alpha, std::vector<int64_t>& df) {
+  df.assign(V, 0);
+  if (V == 0 || N == 0) return;
+  const double cap = std::max<double>(1.0, std::floor(N / 2.0));
+  auto total = [&](double C) {
+    double s = 0;
+    for (int64_t t = 0; t < V; ++t) s += std::min(cap, std::max(1.0, C / std::pow((double)(t + 1), alpha)));
+    return s;
+  };
+  double lo = 0.0, hi = 1.0;
+  while (total(hi) < (double)nnz && hi < 1e30) hi *= 2.0;
+  for (int it = 0; it < 200; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (total(mid) < (double)nnz) lo = mid; else hi = mid;
+  }
+  for (int64_t t = 0; t < V; ++t) {
+    const double x = std::min(cap, std::max(1.0, hi / std::pow((double)(t + 1), alpha)));
+    df[t] = std::max<int64_t>(1, std::min<int64_t>((int64_t)cap, (int64_t)std::llround(x)));
+  }
+}
+
+Plan make_plan(int64_t N, int64_t V, int64_t nnz, double alpha) {
+  Plan p;
+  p.N = N;
+  p.V = V;
+  solve_df(N, V, nnz, alpha, p.df);
+  p.inv_log1m.resize(V);
+  p.idf.resize(V);
+  p.all.resize(V);
+  for (int64_t t = 0; t < V; ++t) {
+    const double pr = (double)p.df[t] / (double)N;
+    p.all[t] = pr >= 1.0;
+    p.inv_log1m[t] = pr >= 1.0 ? 0.0 : 1.0 / std::log1p(-pr);
+    const double d = (double)p.df[t];
+    p.idf[t] = (float)std::log(1.0 + ((double)N - d + 0.5) / (d + 0.5));
+  }
+  return p;
+}
+
+// Walk the postings of term t inside [lo, hi); emit(doc, value).
+template <class F>
+void walk_term(const Plan& p, uint64_t seed, int64_t t, int64_t lo, int64_t hi, F&& emit) {
+  if (lo >= hi) return;
+  const int64_t c0 = lo / kChunk, c1 = (hi + kChunk - 1) / kChunk;
+  for (int64_t c = c0; c < c1; ++c) {
+    Rng rng(stream_seed(seed, t, c));
+    const int64_t base = c * kChunk;
+    const int64_t len = std::min(kChunk, p.N - base);
+    int64_t pos = -1;
+    for (;;) {
+      int64_t gap = 0;
+      if (!p.all[t]) {
+        const double g = std::floor(std::log(rng.unit()) * p.inv_log1m[t]);
+        gap = g >= (double)kChunk ? kChunk : (int64_t)g;
+      }
+      pos += gap + 1;
+      if (pos >= len) break;
+      const uint64_t x = rng.next();
+      const int64_t doc = base + pos;
+      if (doc < lo || doc >= hi) continue;
+      const float u = 0.1f + 0.9f * ((float)(x >> 40) * (1.0f / 16777216.0f));
+      emit(doc, p.idf[t] * u);
+    }
+  }
+}
+
+template <class F>
+void parallel_terms(int64_t V, int nthreads, F&& body) {
+  if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+  nthreads = (int)std::min<int64_t>(nthreads, std::max<int64_t>(V, 1));
+  std::atomic<int64_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const int64_t t0 = next.fetch_add(64);
+      if (t0 >= V) break;
+      for (int64_t t = t0; t < std::min(V, t0 + 64); ++t) body(t);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < nthreads; ++i) th.emplace_back(work);
+  work();
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+int bm25_synth_df(int64_t N, int64_t V, int64_t nnz, double alpha, int64_t* df_out) {
+  if (N <= 0 || V < 0 || nnz < 0 || !df_out) return 1;
+  std::vector<int64_t> df;
+  solve_df(N, V, nnz, alpha, df);
+  std::copy(df.begin(), df.end(), df_out);
+  return 0;
+}
+
+// indptr_out[V+1] of the shard [doc_lo, doc_hi)
+int bm25_synth_count(int64_t N, int64_t V, int64_t nnz, double alpha, uint64_t seed,
+                     int64_t doc_lo, int64_t doc_hi, int nthreads, int64_t* indptr_out) {
+  if (N <= 0 || V < 0 || doc_lo < 0 || doc_hi > N || doc_lo > doc_hi || !indptr_out) return 1;
+  const Plan p = make_plan(N, V, nnz, alpha);
+  std::vector<int64_t> cnt(V, 0);
+  parallel_terms(V, nthreads, [&](int64_t t) {
+    int64_t n = 0;
+    walk_term(p, seed, t, doc_lo, doc_hi, [&](int64_t, float) { ++n; });
+    cnt[t] = n;
+  });
+  indptr_out[0] = 0;
+  for (int64_t t = 0; t < V; ++t) indptr_out[t + 1] = indptr_out[t] + cnt[t];
+  return 0;
+}
+
+// indices are local to the shard (doc - doc_lo)
+int bm25_synth_fill(int64_t N, int64_t V, int64_t nnz, double alpha, uint64_t seed,
+                    int64_t doc_lo, int64_t doc_hi, int nthreads, const int64_t* indptr,
+                    int32_t* indices, float* data) {
+  if (N <= 0 || V < 0 || doc_lo < 0 || doc_hi > N || doc_lo > doc_hi || !indptr) return 1;
+  const Plan p = make_plan(N, V, nnz, alpha);
+  std::atomic<int> bad{0};
+  parallel_terms(V, nthreads, [&](int64_t t) {
+    int64_t o = indptr[t];
+    const int64_t e = indptr[t + 1];
+    walk_term(p, seed, t, doc_lo, doc_hi, [&](int64_t d, float v) {
+      if (o < e) {
+        indices[o] = (int32_t)(d - doc_lo);
+        data[o] = v;
+      }
+      ++o;
+    });
+    if (o != e) bad.store(1);
+  });
+  return bad.load();
+}
+
+// queries[Q][T]: T distinct terms each, P(t) ~ df[t]^beta
+int bm25_synth_queries(int64_t V, const int64_t* df, int64_t Q, int64_t T, double beta,
+                       uint64_t seed, int32_t* out) {
+  if (V <= 0 || T > V || Q < 0 || T < 0 || !df || !out) return 1;
+  std::vector<double> cdf(V);
+  double s = 0;
+  for (int64_t t = 0; t < V; ++t) {
+    s += std::pow((double)std::max<int64_t>(df[t], 0), beta);
+    cdf[t] = s;
+  }
+  for (int64_t q = 0; q < Q; ++q) {
+    Rng rng(stream_seed(seed, -7, q));
+    int32_t* row = out + q * T;
+    for (int64_t i = 0; i < T;) {
+      const double u = (rng.unit() - 1e-300) * s;
+      int64_t t = std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin();
+      if (t >= V) t = V - 1;
+      bool dup = false;
+      for (int64_t j = 0; j < i; ++j) dup |= row[j] == (int32_t)t;
+      if (dup) continue;
+      row[i++] = (int32_t)t;
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,276 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the
+reference's golden vectors.  Bar: top-k doc ids and scores BIT-exact against
+the canonical oracle (same fp32 adds in the same order, same (score desc,
+doc asc) rule); against bm25_native's golden outputs, scores bit-exact and
+ids exact wherever the reference score is untied (tie-aware, tolerance 0)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def _idx(indptr, indices, data, n_docs, shift=None, doc_offset=0):
+    from bm25mi.index import GpuIndex
+    old = os.environ.get("BM25_TILE_SHIFT")
+    if shift is not None:
+        os.environ["BM25_TILE_SHIFT"] = str(shift)
+    try:
+        return GpuIndex(indptr, indices, data, n_docs, doc_offset=doc_offset)
+    finally:
+        if shift is not None:
+            if old is None:
+                os.environ.pop("BM25_TILE_SHIFT")
+            else:
+                os.environ["BM25_TILE_SHIFT"] = old
+
+
+def _exact(a, b):
+    assert a[0].shape == b[0].shape
+    diff = np.nonzero((a[0] != b[0]) | (a[1].view(np.uint32) != b[1].view(np.uint32)))
+    assert diff[0].size == 0, (f"{diff[0].size} mismatches, first at {diff[0][0]},{diff[1][0]}: "
+                               f"gpu {a[0][diff[0][0]][:6]} {a[1][diff[0][0]][:6]} "
+                               f"oracle {b[0][diff[0][0]][:6]} {b[1][diff[0][0]][:6]}")
+
+
+def _rand_index(rng, N, V, dfmax, signed=False, coarse=False):
+    indptr, idx, dat = [0], [], []
+    for t in range(V):
+        df = int(rng.integers(0, min(dfmax, N) + 1))
+        idx.append(np.sort(rng.choice(N, df, replace=False)).astype(np.int32))
+        v = rng.uniform(-2.0 if signed else 0.05, 3.0, df)
+        if coarse:
+            v = np.round(v * 4) / 4
+        dat.append(v.astype(np.float32))
+        indptr.append(indptr[-1] + df)
+    return (np.array(indptr, np.int64), np.concatenate(idx) if idx else np.zeros(0, np.int32),
+            np.concatenate(dat) if dat else np.zeros(0, np.float32))
+
+
+# ---------------------------------------------------------------- golden
+@pytest.mark.parametrize("case", ["q1", "dup", "pad", "batch", "allk"])
+def test_animal_golden_bm25v(gpu, case):
+    import scipy.sparse as sp
+    import bm25_native
+    g = _load("animal.npz")
+    n = int(g["n_docs"])
+    m = sp.csc_matrix((g["data"], g["indices"], g["indptr"]), shape=(n, len(g["indptr"]) - 1))
+    model = bm25_native.BM25v()
+    model.index(m, np.ones(n, np.int32))
+    q, k = g[f"{case}_queries"], int(g[f"{case}_k"])
+    docs, scores = model.search(q, top_k=k)
+    assert docs.dtype == np.int32 and scores.dtype == np.float32 and docs.shape == (len(q), k)
+    bad = oracle.compare_topk(docs, scores, g[f"{case}_docs"], g[f"{case}_scores"],
+                              tied=g[f"{case}_tied"], atol=0.0)
+    assert not bad, bad
+    _exact((docs, scores), oracle.search_c(n, g["indptr"], g["indices"], g["data"], q, k))
+
+
+def test_animal_errors_match_reference(gpu):
+    import scipy.sparse as sp
+    import bm25_native
+    g = _load("animal.npz")
+    m = sp.csc_matrix((g["data"], g["indices"], g["indptr"]), shape=(4, 20))
+    model = bm25_native.BM25v()
+    model.index(m, np.ones(4, np.int32))
+    with pytest.raises(ValueError) as e:
+        model.search(np.array([[20]], np.int32), 1)
+    assert f"ValueError: {e.value}" == str(g["err_token"])
+    with pytest.raises(ValueError) as e:
+        model.search(np.array([[0]], np.int32), 5)
+    assert f"ValueError: {e.value}" == str(g["err_k"])
+    d, s = model.search(np.zeros((0, 4), np.int32), 3)
+    assert d.shape == (0, 0) and str(d.dtype) == str(g["empty_docs_dtype"])
+    d, s = model.search(np.array([[1, 2]], np.int32), 0)
+    assert d.shape == (1, 0) and s.shape == (1, 0)
+
+
+def test_main_demo(gpu):
+    import scipy.sparse as sp
+    import bm25_native
+    from gpu_bm25.common import gpu_execute_query
+    g = _load("main_demo.npz")
+    m = sp.csc_matrix(g["dense"])
+    model = bm25_native.BM25v()
+    model.index(m, np.array([2], np.int32))
+    d, s = model.search(g["queries"], top_k=1)
+    assert d.tolist() == [[1]] and s.tolist() == [[6.0]]
+    idx, w = gpu_execute_query(g["dense"], np.array([0, 1], np.int32), None, None)
+    assert idx.item() == 1 and w.item() == 6.0
+
+
+@pytest.mark.parametrize("k", [1, 10, 100])
+def test_synth_small_golden(gpu, k):
+    g = _load("synth_small.npz")
+    n = int(g["n_docs"])
+    ix = _idx(g["indptr"], g["indices"], g["data"], n)
+    docs, scores = ix.search(g["queries"], k)
+    bad = oracle.compare_topk(docs, scores, g[f"docs_k{k}"], g[f"scores_k{k}"],
+                              tied=g[f"tied_k{k}"], atol=0.0)
+    assert not bad, bad[:4]
+    _exact((docs, scores), oracle.search_c(n, g["indptr"], g["indices"], g["data"],
+                                           g["queries"], k))
+
+
+def test_dense_scores_bit_exact(gpu):
+    g = _load("synth_small.npz")
+    n = int(g["n_docs"])
+    ix = _idx(g["indptr"], g["indices"], g["data"], n)
+    for i, key in ((0, "dense0"), (8, "dense8")):
+        d = ix.scores_dense(g["queries"][i])
+        assert np.array_equal(d.view(np.uint32), g[key].view(np.uint32))
+
+
+# ------------------------------------------------------- synthetic parity
+@pytest.mark.parametrize("shift", [13, 14, 15])
+def test_tile_shifts_random(gpu, shift):
+    rng = np.random.default_rng(shift)
+    N, V = 70_001, 700
+    ip, ix, dt = _rand_index(rng, N, V, 6000)
+    q = rng.integers(-1, V, size=(37, 9)).astype(np.int32)
+    index = _idx(ip, ix, dt, N, shift=shift)
+    for k in (1, 4, 5, 64, 300):
+        _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+
+
+def test_signed_and_tied_values(gpu):
+    rng = np.random.default_rng(11)
+    N, V = 40_000, 300
+    ip, ix, dt = _rand_index(rng, N, V, 8000, signed=True, coarse=True)
+    q = rng.integers(-2, V, size=(50, 6)).astype(np.int32)
+    index = _idx(ip, ix, dt, N)
+    for k in (3, 50, 1000):
+        _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+
+
+def test_zero_fill_and_k_equals_n(gpu):
+    rng = np.random.default_rng(3)
+    N, V = 1000, 50
+    ip, ix, dt = _rand_index(rng, N, V, 5)
+    q = np.array([[1, 2, -1], [-1, -1, -1], [3, 3, 3], [49, 0, 7]], np.int32)
+    index = _idx(ip, ix, dt, N)
+    for k in (10, 200, N):
+        _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+
+
+def test_long_queries_multiple_term_groups(gpu):
+    rng = np.random.default_rng(4)
+    N, V = 30_000, 400
+    ip, ix, dt = _rand_index(rng, N, V, 3000)
+    q = rng.integers(-1, V, size=(9, 45)).astype(np.int32)
+    q[0, :] = 7  # one term 45 times
+    index = _idx(ip, ix, dt, N)
+    _exact(index.search(q, 25), oracle.search_c(N, ip, ix, dt, q, 25))
+
+
+def test_tiny_and_empty_shapes(gpu):
+    ip = np.array([0, 1, 1, 3], np.int32)
+    ix = np.array([0, 0, 2], np.int32)
+    dt = np.array([1.0, 0.5, 2.0], np.float32)
+    index = _idx(ip, ix, dt, 3)
+    q = np.array([[0, 1, 2]], np.int32)
+    _exact(index.search(q, 3), oracle.search_c(3, ip, ix, dt, q, 3))
+    d, s = index.search(np.zeros((2, 0), np.int32), 2)  # T = 0: all zero, smallest ids
+    assert d.tolist() == [[0, 1], [0, 1]] and not s.any()
+    one = _idx(np.array([0, 1], np.int32), np.array([0], np.int32), np.array([3.0], np.float32), 1)
+    assert one.search(np.array([[0]], np.int32), 1)[0].tolist() == [[0]]
+
+
+def test_rescore_path_clustered_tile(gpu):
+    # every high score sits in tile 0, so tile 0 must be rescored exactly
+    N, V = 200_000, 3
+    ip = np.array([0, 5000, 5000 + N // 2, 5000 + N // 2 + 10], np.int64)
+    ix = np.concatenate([np.arange(5000, dtype=np.int32),
+                         np.arange(0, N, 2, dtype=np.int32),
+                         np.arange(10, dtype=np.int32) * 1000]).astype(np.int32)
+    rng = np.random.default_rng(8)
+    dt = np.concatenate([rng.uniform(10, 20, 5000), rng.uniform(0, 1, N // 2),
+                         rng.uniform(0, 30, 10)]).astype(np.float32)
+    index = _idx(ip, ix, dt, N)
+    q = np.array([[0, 1, 2], [1, 0, -1], [2, 2, 1]], np.int32)
+    index.profile_enable(True)
+    for k in (100, 2048):
+        got = index.search(q, k)
+        _exact(got, oracle.search_c(N, ip, ix, dt, q, k))
+        assert index.profile_read()["rescored_tiles_last"] > 0
+
+
+def test_search_device_torch(gpu):
+    import torch
+    g = _load("synth_small.npz")
+    n = int(g["n_docs"])
+    ix = _idx(g["indptr"], g["indices"], g["data"], n)
+    dq = torch.from_numpy(g["queries"]).to("cuda:0")
+    dd = torch.empty((dq.shape[0], 10), dtype=torch.int32, device="cuda:0")
+    ds = torch.empty((dq.shape[0], 10), dtype=torch.float32, device="cuda:0")
+    stream = torch.cuda.current_stream()
+    ix.search_device(dq, 10, dd, ds, stream)
+    torch.cuda.synchronize()
+    _exact((dd.cpu().numpy(), ds.cpu().numpy()),
+           oracle.search_c(n, g["indptr"], g["indices"], g["data"], g["queries"], 10))
+
+
+def test_sharded_merge_equals_single_index(gpu):
+    import torch
+    from bm25mi import synth
+    from bm25mi.index import GpuIndex, merge_topk_device
+    cfg = synth.Config("t", 300_000, 5000, 2_000_000, 64, 8, 100)
+    full = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    ref = oracle.search_c(cfg.n_docs, *full, q, cfg.k)
+    W = 3
+    dq = torch.from_numpy(q).cuda()
+    outs_d = torch.empty((W, len(q), cfg.k), dtype=torch.int32, device="cuda")
+    outs_s = torch.empty((W, len(q), cfg.k), dtype=torch.float32, device="cuda")
+    shards = []
+    for r in range(W):
+        lo, hi = synth.shard_bounds(cfg.n_docs, W, r)
+        ip, ix, dt = synth.make_index(cfg, lo, hi)
+        sh = GpuIndex(ip, ix, dt, hi - lo, doc_offset=lo)
+        shards.append(sh)
+        sh.search_device(dq, cfg.k, outs_d[r], outs_s[r], torch.cuda.current_stream())
+    md = torch.empty((len(q), cfg.k), dtype=torch.int32, device="cuda")
+    ms = torch.empty((len(q), cfg.k), dtype=torch.float32, device="cuda")
+    merge_topk_device(0, outs_d, outs_s, W, len(q), cfg.k, md, ms, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)
+
+
+def test_config2_full_parity(gpu):
+    from bm25mi import synth
+    cfg = synth.CONFIGS["c2"]
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    index = _idx(ip, ix, dt, cfg.n_docs)
+    _exact(index.search(q, cfg.k), oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k))
+
+
+def test_config3_full_index_subset_parity(gpu):
+    """The headline 10M-doc / 200k-vocab / 640M-posting index, k=100: a
+    32-query subset checked exactly against the C oracle, and the whole
+    1024-query batch checked for size-independent properties."""
+    from bm25mi import synth
+    cfg = synth.CONFIGS["c3"]
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    index = _idx(ip, ix, dt, cfg.n_docs)
+    docs, scores = index.search(q, cfg.k)
+    sub = np.arange(0, 1024, 32)
+    _exact((docs[sub], scores[sub]), oracle.search_c(cfg.n_docs, ip, ix, dt, q[sub], cfg.k))
+    # whole batch: sorted, unique ids in range, ties ordered by id
+    assert np.all(np.diff(scores, axis=1) <= 0)
+    assert all(len(set(r)) == cfg.k for r in docs.tolist())
+    assert docs.min() >= 0 and docs.max() < cfg.n_docs
+    eq = np.diff(scores, axis=1) == 0
+    assert np.all(np.diff(docs, axis=1)[eq] > 0)
+    # idempotent: a second search returns the same bits
+    d2, s2 = index.search(q, cfg.k)
+    assert np.array_equal(d2, docs) and np.array_equal(s2.view(np.uint32), scores.view(np.uint32))
