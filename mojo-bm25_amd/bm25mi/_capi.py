@@ -23,6 +23,17 @@ if not os.path.exists(LIB):
         f"libbm25mi.so not found at {LIB}: run __graft_entry__.build() "
         "(python mojo-bm25_amd/bm25mi/build.py) — there is no CPU fallback")
 
+# One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64
+# (SONAME libamdhip64.so.7, loaded through its RPATH under a different NEEDED
+# name), so if libbm25mi.so bound /opt/rocm's copy first, torch would later load
+# a second runtime that sees no GPU.  Importing torch first makes the dynamic
+# linker satisfy libbm25mi's NEEDED libamdhip64.so.7 with the copy already
+# mapped, so device pointers and streams are shared with torch.
+try:  # pragma: no cover - depends on the environment
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 lib = ctypes.CDLL(LIB)
 
 _P = ctypes.c_void_p
