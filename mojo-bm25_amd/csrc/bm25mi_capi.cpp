@@ -79,6 +79,7 @@ namespace {
 
 void free_ws(Workspace& ws) {
   hipFree(ws.cand);
+  hipFree(ws.theta);
   hipFree(ws.cand2);
   hipFree(ws.flag_tiles);
   hipFree(ws.nflag);
@@ -95,6 +96,7 @@ int ensure_ws(bm25_index* h, int64_t Q, int k) {
   free_ws(ws);
   const int64_t mf = maxflag_for((int)kk, h->ix.ntiles);
   HIP_TRY(hipMalloc(&ws.cand, sizeof(uint64_t) * q * h->ix.ntiles * kTileM), "hipMalloc(cand)");
+  HIP_TRY(hipMalloc(&ws.theta, sizeof(uint64_t) * q), "hipMalloc(theta)");
   HIP_TRY(hipMalloc(&ws.cand2, sizeof(uint64_t) * q * mf * kk), "hipMalloc(cand2)");
   HIP_TRY(hipMalloc(&ws.flag_tiles, sizeof(int32_t) * q * mf), "hipMalloc(flag_tiles)");
   HIP_TRY(hipMalloc(&ws.nflag, sizeof(int32_t) * q), "hipMalloc(nflag)");
@@ -161,7 +163,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   if (rc) return rc;
   EventPair* ev = next_events(h);
   if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
-  HIP_TRY(launch_score_tiles(h->ix, d_queries, Q, T, h->ws, st), "score_tiles launch");
+  HIP_TRY(launch_score_tiles(h->ix, d_queries, Q, T, k, h->ws, st), "score_tiles launch");
   if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
   HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, h->ws, d_docs, d_scores, st), "select launch");
   if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
@@ -258,8 +260,10 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
   const int64_t rel_elems = n_terms * (ntiles + 1);
   TRYC(hipMalloc(&ix.indptr, sizeof(int64_t) * (n_terms + 1)), "hipMalloc(indptr)");
   TRYC(hipMalloc(&ix.rel, sizeof(uint32_t) * std::max<int64_t>(rel_elems, 1)), "hipMalloc(rel)");
-  TRYC(hipMalloc(&ix.ldoc, sizeof(uint16_t) * std::max<int64_t>(nnz, 1)), "hipMalloc(ldoc)");
-  TRYC(hipMalloc(&ix.val, sizeof(float) * std::max<int64_t>(nnz, 1)), "hipMalloc(val)");
+  TRYC(hipMalloc(&ix.ldoc, sizeof(uint16_t) * (nnz + kPostingPad)), "hipMalloc(ldoc)");
+  TRYC(hipMalloc(&ix.val, sizeof(float) * (nnz + kPostingPad)), "hipMalloc(val)");
+  TRYC(hipMemsetAsync(ix.ldoc + nnz, 0, sizeof(uint16_t) * kPostingPad, h->stream), "hipMemset");
+  TRYC(hipMemsetAsync(ix.val + nnz, 0, sizeof(float) * kPostingPad, h->stream), "hipMemset");
   TRYC(hipMalloc(&d_indices, sizeof(int32_t) * std::max<int64_t>(nnz, 1)), "hipMalloc(indices)");
   TRYC(hipMalloc(&d_err, sizeof(int32_t)), "hipMalloc(err)");
   h->device_bytes = (int64_t)(sizeof(int64_t) * (n_terms + 1) + sizeof(uint32_t) * rel_elems +

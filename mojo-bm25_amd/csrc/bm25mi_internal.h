@@ -2,10 +2,14 @@
 // (bm25mi_capi.cpp) and the gfx950 kernels (bm25mi_kernels.hip).
 //
 // Device layout of one index:
-//   val   f32 [nnz]          the CSC `data` array, unchanged order (term-major,
+//   val   f32 [nnz+pad]      the CSC `data` array, unchanged order (term-major,
 //                            doc-ascending inside a term)
-//   ldoc  u16 [nnz]          doc id modulo the tile size (doc & (D-1)); the
+//   ldoc  u16 [nnz+pad]      LDS slot of the doc inside its tile: the doc's
+//                            tile-local id (doc & (D-1)) through the fixed
+//                            accumulator permutation acc_slot() below; the
 //                            tile of a posting is implied by its position
+//                            (pad: kPostingPad elements so 4-posting vector
+//                            loads of a segment's last row stay in bounds)
 //   indptr i64 [V+1]         CSC column pointers
 //   rel   u32 [V][ntiles+1]  rel[t][j] = first posting of term t whose doc is
 //                            in tile j or later, relative to indptr[t]
@@ -41,6 +45,9 @@ constexpr int kTileM = 4;
 constexpr int kMaxK = 4096;
 // Merge kernel LDS: number of u64 keys sorted at once.
 constexpr int kMergeP = 8192;
+// One full posting row (4 postings x 1024 lanes) past the end, so row loads
+// never need clamping (their out-of-segment lanes are masked, not skipped).
+constexpr int64_t kPostingPad = 4 * 1024 + 8;
 
 struct DevIndex {
   int device = 0;
@@ -56,6 +63,7 @@ struct DevIndex {
 struct Workspace {
   int64_t cap_q = 0, cap_k = 0;
   uint64_t* cand = nullptr;      // [Q][ntiles][kTileM]
+  uint64_t* theta = nullptr;     // [Q] k-th key of the sample tiles' candidates
   uint64_t* cand2 = nullptr;     // [Q][maxflag][k]  exact top-k of re-scored tiles
   int32_t* flag_tiles = nullptr; // [Q][maxflag]
   int32_t* nflag = nullptr;      // [Q]
@@ -65,6 +73,14 @@ struct Workspace {
 
 // Flag slots per query: a flagged tile holds kTileM keys of the top-(k-1), so
 // at most (k-1)/kTileM tiles (and never more than the tiles that exist).
+// Accumulator layout of a tile of D = 2^S docs: tile-local doc d belongs to
+// selection thread t = d / 32 (entry e = d % 32, so lane order == doc order)
+// and lives at float index ((e/4) * NT + t) * 4 + e % 4 with NT = D / 32:
+// the selection's float4 reads (j*NT + t) are then conflict-free.
+__host__ __device__ inline uint32_t acc_slot(uint32_t d, int S) {
+  return ((d & 28u) << (S - 5)) | ((d >> 3) & ~3u) | (d & 3u);
+}
+
 inline int64_t maxflag_for(int k, int64_t ntiles) {
   const int64_t m = (k + kTileM - 1) / kTileM;
   return m < ntiles ? m : (ntiles > 0 ? ntiles : 1);
@@ -73,9 +89,11 @@ inline int64_t maxflag_for(int k, int64_t ntiles) {
 // Kernel launchers (bm25mi_kernels.hip).  All enqueue on `stream`.
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,
                                int32_t* d_err, hipStream_t stream);
-// Score pass: every (tile, query) -> top kTileM keys per tile.
+// Score pass: every (tile, query) -> kTileM candidate keys per tile
+// (sample tiles: exact top-kTileM; other tiles: the keys above the sample's
+// k-th key, or their exact top-kTileM when more than kTileM pass).
 hipError_t launch_score_tiles(const DevIndex& ix, const int32_t* d_queries,
-                              int64_t Q, int64_t T, const Workspace& ws,
+                              int64_t Q, int64_t T, int k, const Workspace& ws,
                               hipStream_t stream);
 // Merge + rescore + final merge.
 hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries,

@@ -6,27 +6,35 @@
 // and its CPU scorer (bm25_native.py:149-158, 204-214) with a doc-tiled
 // sparse design:
 //
-//   score_tiles   one workgroup per (doc tile, query): gathers the query's
-//                 posting segments inside the tile (coalesced reads of the
-//                 CSC `data` + u16 local doc ids), scatter-adds them into an
-//                 fp32 LDS accumulator term by term in query order (the exact
-//                 fp32 arithmetic of scipy csc_matvec, bm25_native.py:152),
-//                 then extracts the tile's top-kTileM keys with wave64
-//                 shuffle/ballot argmax rounds.
+//   score_tiles<SAMPLE>  one workgroup per (sample doc tile, query): gathers
+//                 the query's posting segments inside the tile (row-uniform,
+//                 4 postings per lane: u16x4 doc ids + f32x4 scores), adds them
+//                 into an fp32 LDS accumulator term by term in query order
+//                 (the exact fp32 arithmetic of scipy csc_matvec,
+//                 bm25_native.py:152), then extracts the tile's exact top-4
+//                 keys with wave64 DPP argmax rounds.
+//   theta         per query, the k-th best sample candidate: a lower bound of
+//                 the final k-th key.
+//   score_tiles<REST>    every other tile: same accumulation, then a compare
+//                 against theta; the (typically 0-2) keys above it are
+//                 emitted, and only a tile with more than 4 runs the argmax.
 //   merge         one workgroup per query: bitonic-sorts the per-tile
 //                 candidates in LDS, picks the top-k and flags the (rare)
-//                 tiles whose kTileM-th candidate beats the k-th key.
+//                 tiles whose 4th candidate beats the k-th key.
 //   rescore       persistent: exact top-k of each flagged tile.
 //   merge(final)  merges the exact lists of flagged tiles.
 // The result is exactly the top-k under (score desc, doc asc) of the dense
 // score vector, with untouched documents scoring 0.
 #include "bm25mi_internal.h"
 
+#include <cstdlib>
+
 namespace bm25mi {
 
 constexpr int kTG = 16;  // query terms staged in LDS per group
-constexpr int kR = 8;    // postings held in registers per thread per chunk
 constexpr int kE = 32;   // accumulator entries owned by a thread in selection
+
+enum Phase { kAll = 0, kSample = 1, kRest = 2 };
 
 struct IndexArgs {
   const int64_t* indptr;
@@ -41,37 +49,66 @@ static IndexArgs args_of(const DevIndex& ix) {
 }
 
 struct TileShared {
-  int64_t base[kTG];        // global posting index = base[s] + concat position
-  uint32_t start[kTG + 1];  // prefix of segment lengths
-  uint32_t red[2][16];      // per-wave argmax values, double-buffered
+  int64_t abeg[kTG];          // a term's first posting in the tile, aligned down to 4
+  uint32_t off[kTG];          // first posting - abeg (0..3)
+  uint32_t len[kTG];          // postings of the term in the tile
+  uint32_t rstart[kTG + 1];   // prefix of row counts
+  uint32_t red[2][16];        // per-wave argmax values, double-buffered
+  int32_t nsel;               // keys emitted by the threshold pass
   int32_t item;
 };
 
+__device__ __forceinline__ uint32_t sgpr(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ int64_t sgpr64(int64_t v) {
+  const uint32_t lo = sgpr((uint32_t)v), hi = sgpr((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Max over the 64 lanes of a wave: DPP inside each 16-lane row, then the four
+// row results through SGPRs.
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
-    v = v > w ? v : w;
-  }
-  return v;
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return max(max(a, b), max(c, d));
 }
 
 // ---------------------------------------------------------------------------
 // Scatter phase: acc[d] = sum over query terms (in order) of the term's score
 // for doc d of this tile.  Replaces doc_toks[:, query].sum(axis=1)
 // (bm25_native.py:152 -> scipy csc_matvec): same fp32 adds, same order per doc.
+//
+// Each term's segment is cut into rows of 4*NT postings aligned down to a
+// multiple of 4; lane t of a row loads postings [4t, 4t+4) of it as one u16x4
+// (accumulator slots, acc_slot() applied at build time) and one f32x4 from a
+// block-uniform base (SGPR base + lane offset).  A row belongs to one term, so
+// a barrier between rows of different terms keeps the per-document add order;
+// inside a term every doc occurs once, so plain LDS read-add-writes never
+// race.  Lanes outside the segment are redirected to a private dummy slot
+// (acc[D + lane]) instead of branching around their LDS accesses.
 // ---------------------------------------------------------------------------
-template <int S>
+template <int S, int kRB = 4>
 __device__ __forceinline__ void accumulate_tile(const IndexArgs& a, int64_t tile,
                                                 const int32_t* __restrict__ qterms,
-                                                int T, float* acc, TileShared& sm) {
+                                                int T, float* acc, TileShared& sm,
+                                                int mode = 0) {
   constexpr int D = 1 << S;
   constexpr int NT = D / kE;
+  constexpr uint32_t RW = 4 * NT;  // postings per row
   const int tid = threadIdx.x;
+  const uint32_t dummy = D + (tid & 63);
 
   float4* acc4 = reinterpret_cast<float4*>(acc);
+  if (!(mode & 8)) {
 #pragma unroll
-  for (int j = 0; j < kE / 4; ++j) acc4[j * NT + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < kE / 4; ++j) acc4[j * NT + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (tid == 0) sm.nsel = 0;
 
   for (int g0 = 0; g0 < T; g0 += kTG) {
     const int ng = min(kTG, T - g0);
@@ -86,102 +123,125 @@ __device__ __forceinline__ void accumulate_tile(const IndexArgs& a, int64_t tile
         lo = a.indptr[term] + r0;
         len = r1 - r0;
       }
-      sm.base[tid] = lo;
-      sm.start[tid + 1] = len;
+      sm.abeg[tid] = lo & ~3ll;
+      sm.off[tid] = (uint32_t)(lo & 3);
+      sm.len[tid] = len;
+      sm.rstart[tid + 1] = len ? (uint32_t)(((lo & 3) + len + RW - 1) / RW) : 0u;
     }
     __syncthreads();
     if (tid == 0) {
       uint32_t s = 0;
-      sm.start[0] = 0;
+      sm.rstart[0] = 0;
       for (int i = 0; i < ng; ++i) {
-        const uint32_t len = sm.start[i + 1];
-        sm.base[i] -= (int64_t)s;
-        s += len;
-        sm.start[i + 1] = s;
+        s += sm.rstart[i + 1];
+        sm.rstart[i + 1] = s;
       }
     }
     __syncthreads();
-    const uint32_t total = sm.start[ng];
-    for (uint32_t cb = 0; cb < total; cb += NT * kR) {
-      // 1) positions -> global posting indices (no memory traffic)
-      int64_t gidx[kR];
-      int sg[kR];
-      int s = 0;
+    const uint32_t R = (mode & 4) ? 0u : sgpr(sm.rstart[ng]);
+    int s = 0;          // term of the current row (block-uniform)
+    int last_s = -1;    // term of the last added row
+    for (uint32_t rb = 0; rb < R; rb += kRB) {
+      ushort4 ld[kRB];
+      float4 v[kRB];
+      int32_t i0[kRB];
+      int rs[kRB];
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        uint32_t P = cb + r * NT + tid;
-        sg[r] = P < total ? 0 : -1;
-        P = P < total ? P : total - 1;
-        while (s + 1 < ng && P >= sm.start[s + 1]) ++s;
-        sg[r] = sg[r] < 0 ? -1 : s;
-        gidx[r] = sm.base[s] + (int64_t)P;
+      for (int b = 0; b < kRB; ++b) {
+        const uint32_t row = rb + b;
+        rs[b] = -1;
+        if (row < R) {
+          while (row >= sgpr(sm.rstart[s + 1])) ++s;
+          const uint32_t rr = row - sgpr(sm.rstart[s]);
+          const int64_t A0 = sgpr64(sm.abeg[s]) + (int64_t)rr * RW;
+          ld[b] = reinterpret_cast<const ushort4*>(a.ldoc + A0)[tid];
+          v[b] = reinterpret_cast<const float4*>(a.val + A0)[tid];
+          i0[b] = (int32_t)(rr * RW) + 4 * tid - (int32_t)sgpr(sm.off[s]);
+          rs[b] = s;
+        }
       }
-      // 2) issue every load of the chunk before the first use
-      uint32_t ld[kR];
-      float v[kR];
+      if (mode & 2) {
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        ld[r] = a.ldoc[gidx[r]];
-        v[r] = a.val[gidx[r]];
+        for (int b = 0; b < kRB; ++b)
+          asm volatile("" ::"v"(ld[b].x), "v"(ld[b].w), "v"(v[b].x), "v"(v[b].w));
+        continue;
       }
-      // 3) LDS adds, one term after the other (a doc occurs once per term, so
-      //    within a term the adds commute; across terms the barrier keeps
-      //    query order, bm25_native.py:152 / csc_matvec)
-      const uint32_t ce = cb + NT * kR;
-      for (int s2 = 0; s2 < ng; ++s2) {
-        if (sm.start[s2 + 1] <= cb || sm.start[s2] >= ce) continue;  // block-uniform
 #pragma unroll
-        for (int r = 0; r < kR; ++r)
-          if (sg[r] == s2) atomicAdd(&acc[ld[r]], v[r]);
-        __syncthreads();
+      for (int b = 0; b < kRB; ++b) {
+        if (rs[b] < 0) break;
+        if (rs[b] != last_s) {
+          if (last_s >= 0) __syncthreads();  // previous term's adds complete
+          last_s = rs[b];
+        }
+        const uint32_t len = sgpr(sm.len[rs[b]]);
+        const uint32_t d0 = (uint32_t)(i0[b] + 0) < len ? (uint32_t)ld[b].x : dummy;
+        const uint32_t d1 = (uint32_t)(i0[b] + 1) < len ? (uint32_t)ld[b].y : dummy;
+        const uint32_t d2 = (uint32_t)(i0[b] + 2) < len ? (uint32_t)ld[b].z : dummy;
+        const uint32_t d3 = (uint32_t)(i0[b] + 3) < len ? (uint32_t)ld[b].w : dummy;
+        // four distinct docs of one term (or the dummy slot): read all, write all
+        const float x0 = acc[d0], x1 = acc[d1], x2 = acc[d2], x3 = acc[d3];
+        acc[d0] = x0 + v[b].x;
+        acc[d1] = x1 + v[b].y;
+        acc[d2] = x2 + v[b].z;
+        acc[d3] = x3 + v[b].w;
       }
     }
   }
   __syncthreads();
 }
 
+// Load this thread's 32 accumulator entries (entry e = tile-local doc
+// tid*32 + e), conflict-free float4 reads.
+template <int S>
+__device__ __forceinline__ void load_entries(const float* acc, float (&fv)[kE]) {
+  constexpr int NT = (1 << S) / kE;
+  const float4* acc4 = reinterpret_cast<const float4*>(acc);
+#pragma unroll
+  for (int j = 0; j < kE / 4; ++j) {
+    const float4 f = acc4[j * NT + threadIdx.x];
+    fv[j * 4 + 0] = f.x;
+    fv[j * 4 + 1] = f.y;
+    fv[j * 4 + 2] = f.z;
+    fv[j * 4 + 3] = f.w;
+  }
+}
+
+// Order-preserving u32 keys of the entries (0 = past n_docs).
+template <int S>
+__device__ __forceinline__ void make_keys(const float (&fv)[kE], int64_t tile, int64_t n_docs,
+                                          uint32_t (&key)[kE]) {
+  constexpr int D = 1 << S;
+  const int64_t doc0 = tile * D + (int64_t)threadIdx.x * kE;
+#pragma unroll
+  for (int e = 0; e < kE; ++e) key[e] = score_key(fv[e]);
+  if (doc0 + kE > n_docs) {
+#pragma unroll
+    for (int e = 0; e < kE; ++e)
+      if (doc0 + e >= n_docs) key[e] = 0;
+  }
+}
+
 // ---------------------------------------------------------------------------
-// Selection phase: the m best keys of the tile, best first, written to out[].
-// Thread t owns docs [t*kE, t*kE + kE) of the tile, so "first wave, first
-// lane, first entry" among equal scores is the smallest doc id.
+// Exact selection: the m best keys of the tile, best first, into out[0..m).
+// Thread t owns docs [t*32, t*32+32), so "first wave, first lane, first entry"
+// among equal scores is the smallest doc id.
 // ---------------------------------------------------------------------------
 template <int S>
-__device__ __forceinline__ void select_tile(const float* acc, int64_t tile, int64_t n_docs,
-                                            int m, uint64_t* __restrict__ out,
-                                            TileShared& sm) {
+__device__ __forceinline__ void select_tile(uint32_t (&key)[kE], int64_t tile, int m,
+                                            uint64_t* __restrict__ out, TileShared& sm) {
   constexpr int D = 1 << S;
   constexpr int NT = D / kE;
   constexpr int NW = NT / 64;
-  constexpr int C4 = kE / 4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float4* acc4 = reinterpret_cast<const float4*>(acc);
-  const int swz = tid & 7;  // rotate chunk order across lanes: spreads LDS banks
   const int64_t doc0 = tile * D + (int64_t)tid * kE;
-
-  uint32_t key[kE];
-#pragma unroll
-  for (int j = 0; j < C4; ++j) {
-    const float4 f = acc4[tid * C4 + (j ^ swz)];
-    key[j * 4 + 0] = score_key(f.x);
-    key[j * 4 + 1] = score_key(f.y);
-    key[j * 4 + 2] = score_key(f.z);
-    key[j * 4 + 3] = score_key(f.w);
-  }
-  if (doc0 + kE > n_docs) {
-#pragma unroll
-    for (int j = 0; j < C4; ++j)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (doc0 + ((j ^ swz) * 4 + c) >= n_docs) key[j * 4 + c] = 0;
-  }
   uint32_t lmax = 0;
 #pragma unroll
-  for (int i = 0; i < kE; ++i) lmax = lmax > key[i] ? lmax : key[i];
+  for (int i = 0; i < kE; ++i) lmax = max(lmax, key[i]);
 
   for (int r = 0; r < m; ++r) {
     const uint32_t wm = wave_max_u32(lmax);
     const unsigned long long bal = __ballot(lmax == wm);
-    const int wl = __ffsll(bal) - 1;
+    const int wl = (int)__builtin_ctzll(bal);
     if (lane == 0) sm.red[r & 1][wave] = wm;
     __syncthreads();
     uint32_t bm = 0;
@@ -196,46 +256,116 @@ __device__ __forceinline__ void select_tile(const float* acc, int64_t tile, int6
       continue;
     }
     if (wave == ws && lane == wl) {
-      int eb = kE;
+      int eb = 0;
 #pragma unroll
-      for (int j = 0; j < C4; ++j)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int e = (j ^ swz) * 4 + c;
-          if (key[j * 4 + c] == bm && e < eb) eb = e;
-        }
+      for (int e = kE - 1; e >= 0; --e)
+        if (key[e] == bm) eb = e;
       out[r] = ((uint64_t)bm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(doc0 + eb));
       lmax = 0;
 #pragma unroll
-      for (int j = 0; j < C4; ++j)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if ((j ^ swz) * 4 + c == eb) key[j * 4 + c] = 0;
-          lmax = lmax > key[j * 4 + c] ? lmax : key[j * 4 + c];
-        }
+      for (int e = 0; e < kE; ++e) {
+        key[e] = e == eb ? 0u : key[e];
+        lmax = max(lmax, key[e]);
+      }
     }
   }
 }
 
-// One workgroup per (tile, query); blocks are dealt round-robin over the 8
-// XCDs (b % 8), so block b maps to item (b % 8) * per + b / 8: each XCD walks
-// its own contiguous run of tiles, all queries of a tile back to back, and the
-// tile's hot posting segments stay in that XCD's L2.
+// Threshold emission (REST tiles): write the keys > theta (at most kTileM;
+// slots past the count are zeroed) and return the block-wide count; above
+// kTileM the caller runs the exact selection instead.  The test runs on the
+// fp32 sums directly (one compare per entry); only a lane holding theta's
+// exact score compares doc ids.  Accumulators are never -0.0 (a sum that
+// starts at +0.0 cannot produce it) and docs past n_docs hold 0.0, which can
+// only pass when theta's score is negative — those are masked explicitly.
 template <int S>
-__global__ __launch_bounds__((1 << S) / kE) void score_tiles_kernel(
-    IndexArgs a, const int32_t* __restrict__ queries, int32_t Q, int32_t T,
-    uint64_t* __restrict__ cand) {
-  __shared__ __attribute__((aligned(16))) float acc[1 << S];
-  __shared__ TileShared sm;
-  const int64_t nitems = a.ntiles * (int64_t)Q;
+__device__ __forceinline__ int emit_above(const float (&fv)[kE], int64_t tile, int64_t n_docs,
+                                          uint64_t theta, uint64_t* __restrict__ out,
+                                          TileShared& sm) {
+  constexpr int D = 1 << S;
+  const int tid = threadIdx.x;
+  const float th = key_score((uint32_t)(theta >> 32));
+  const uint32_t th_doc = 0xFFFFFFFFu - (uint32_t)theta;
+  const int64_t doc0 = tile * D + (int64_t)tid * kE;
+  const int64_t lim_hi = n_docs - doc0;  // entries e >= lim_hi are past n_docs
+  int c = 0;
+  bool tie = false;
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    c += fv[e] > th;
+    tie |= fv[e] == th;
+  }
+  if (tie || lim_hi < kE) {  // rare: exact per-entry rule
+    const int64_t lim_tie = (int64_t)th_doc - doc0;  // ties pass for e < lim_tie
+    c = 0;
+#pragma unroll
+    for (int e = 0; e < kE; ++e)
+      c += (e < lim_hi) & ((fv[e] > th) | ((fv[e] == th) & (e < lim_tie)));
+  }
+  if (c > 0) {
+    const int64_t lim_tie = (int64_t)th_doc - doc0;
+    int pos = atomicAdd(&sm.nsel, c);
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const bool pass = (e < lim_hi) & ((fv[e] > th) | ((fv[e] == th) & (e < lim_tie)));
+      if (pass) {
+        if (pos < kTileM)
+          out[pos] = ((uint64_t)score_key(fv[e]) << 32) |
+                     (uint64_t)(0xFFFFFFFFu - (uint32_t)(doc0 + e));
+        ++pos;
+      }
+    }
+  }
+  __syncthreads();
+  const int n = sm.nsel;
+  if (n < kTileM && tid < kTileM - n) out[n + tid] = 0;
+  return n;
+}
+
+// Work item -> (tile, query).  Blocks are dealt round-robin over the 8 XCDs
+// (b % 8), so block b runs item (b % 8) * per + b / 8: each XCD walks its own
+// contiguous run of tiles, all queries of a tile back to back, and the tile's
+// hot posting segments stay in that XCD's L2.
+template <int PH>
+__device__ __forceinline__ bool item_of(int64_t ntiles, int64_t Q, int P, int64_t& tile,
+                                        int64_t& q) {
+  const int64_t nS = (ntiles + P - 1) / P;
+  const int64_t nt = PH == kAll ? ntiles : (PH == kSample ? nS : ntiles - nS);
+  const int64_t nitems = nt * Q;
   const int64_t per = (nitems + 7) >> 3;
   const int64_t b = blockIdx.x;
   const int64_t item = (b & 7) * per + (b >> 3);
-  if (item >= nitems) return;
-  const int64_t tile = item / Q;
-  const int64_t q = item - tile * Q;
-  accumulate_tile<S>(a, tile, queries + q * T, T, acc, sm);
-  select_tile<S>(acc, tile, a.n_docs, kTileM, cand + (q * a.ntiles + tile) * kTileM, sm);
+  if (item >= nitems) return false;
+  const int64_t ti = item / Q;
+  q = item - ti * Q;
+  if (PH == kAll) tile = ti;
+  else if (PH == kSample) tile = ti * P;
+  else tile = (ti / (P - 1)) * P + (ti % (P - 1)) + 1;
+  return true;
+}
+
+template <int S, int PH, int RB>
+__global__ __launch_bounds__((1 << S) / kE) void score_tiles_kernel(
+    IndexArgs a, const int32_t* __restrict__ queries, int32_t Q, int32_t T, int32_t P,
+    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int mode) {
+  __shared__ __attribute__((aligned(16))) float acc[(1 << S) + 64];
+  __shared__ TileShared sm;
+  int64_t tile, q;
+  if (!item_of<PH>(a.ntiles, Q, P, tile, q)) return;
+  accumulate_tile<S, RB>(a, tile, queries + q * T, T, acc, sm, mode);
+  uint64_t* out = cand + (q * a.ntiles + tile) * kTileM;
+  if (mode & 1) {  // ablation: no selection
+    if (threadIdx.x == 0) out[0] = __float_as_uint(acc[0]);
+    return;
+  }
+  float fv[kE];
+  load_entries<S>(acc, fv);
+  if (PH == kRest) {
+    if (emit_above<S>(fv, tile, a.n_docs, theta[q], out, sm) <= kTileM) return;
+  }
+  uint32_t key[kE];
+  make_keys<S>(fv, tile, a.n_docs, key);
+  select_tile<S>(key, tile, kTileM, out, sm);
 }
 
 // Exact top-k of each flagged tile; persistent, pulls items from the queue
@@ -244,7 +374,7 @@ template <int S>
 __global__ __launch_bounds__((1 << S) / kE) void rescore_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t k,
     int64_t maxflag, Workspace ws) {
-  __shared__ __attribute__((aligned(16))) float acc[1 << S];
+  __shared__ __attribute__((aligned(16))) float acc[(1 << S) + 64];
   __shared__ TileShared sm;
   const int32_t n_items = ws.counters[0];
   for (;;) {
@@ -257,27 +387,34 @@ __global__ __launch_bounds__((1 << S) / kE) void rescore_kernel(
     const int64_t q = code / maxflag;
     const int64_t tile = ws.flag_tiles[code];
     accumulate_tile<S>(a, tile, queries + q * T, T, acc, sm);
-    select_tile<S>(acc, tile, a.n_docs, k, ws.cand2 + (int64_t)code * k, sm);
+    float fv[kE];
+    load_entries<S>(acc, fv);
+    uint32_t key[kE];
+    make_keys<S>(fv, tile, a.n_docs, key);
+    select_tile<S>(key, tile, k, ws.cand2 + (int64_t)code * k, sm);
   }
 }
 
 template <int S>
 __global__ __launch_bounds__((1 << S) / kE) void scores_dense_kernel(
     IndexArgs a, const int32_t* __restrict__ query, int32_t T, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float acc[1 << S];
+  __shared__ __attribute__((aligned(16))) float acc[(1 << S) + 64];
   __shared__ TileShared sm;
   constexpr int D = 1 << S;
   constexpr int NT = D / kE;
   const int64_t tile = blockIdx.x;
   accumulate_tile<S>(a, tile, query, T, acc, sm);
-  const int64_t d0 = tile * D;
-  if (d0 + D <= a.n_docs) {
+  const float4* acc4 = reinterpret_cast<const float4*>(acc);
+  const int64_t d0 = tile * D + (int64_t)threadIdx.x * kE;  // this thread's 32 docs
+  if (d0 + kE <= a.n_docs) {
     float4* o4 = reinterpret_cast<float4*>(out + d0);
-    const float4* acc4 = reinterpret_cast<const float4*>(acc);
 #pragma unroll
-    for (int j = 0; j < kE / 4; ++j) o4[j * NT + threadIdx.x] = acc4[j * NT + threadIdx.x];
+    for (int j = 0; j < kE / 4; ++j) o4[j] = acc4[j * NT + threadIdx.x];
   } else {
-    for (int64_t e = threadIdx.x; d0 + e < a.n_docs; e += NT) out[d0 + e] = acc[e];
+    for (int e = 0; e < kE && d0 + e < a.n_docs; ++e) {
+      const float4 f = acc4[(e >> 2) * NT + threadIdx.x];
+      out[d0 + e] = (e & 3) == 0 ? f.x : (e & 3) == 1 ? f.y : (e & 3) == 2 ? f.z : f.w;
+    }
   }
 }
 
@@ -302,7 +439,7 @@ __global__ __launch_bounds__(256) void build_tables_kernel(
       const int32_t dp = p > a0 ? indices[p - 1] : -1;
       const bool ok = d >= 0 && (int64_t)d < n_docs && d > dp;
       if (!ok) atomicOr(err, 1);
-      ldoc[p] = (uint16_t)((uint32_t)d & mask);
+      ldoc[p] = (uint16_t)acc_slot((uint32_t)d & mask, S);
       if (ok) {
         const int64_t tp = dp >= 0 ? ((int64_t)dp >> S) : -1;
         const int64_t tc = (int64_t)d >> S;
@@ -381,6 +518,14 @@ struct SrcFirst {
   __device__ uint64_t operator()(int64_t i) const { return c[i]; }
 };
 
+struct SrcSample {  // the kTileM slots of every P-th tile
+  const uint64_t* c;
+  int P;
+  __device__ uint64_t operator()(int64_t i) const {
+    return c[(i / kTileM) * P * kTileM + (i % kTileM)];
+  }
+};
+
 struct SrcFinal {
   const uint64_t* c;      // this query's [ntiles][M] candidates
   const uint64_t* c2;     // this query's flagged tiles' exact lists, contiguous
@@ -406,6 +551,19 @@ struct SrcLists {
     return make_key(scores[o], (uint32_t)docs[o]);
   }
 };
+
+// theta[q] = k-th best key among the sample tiles' candidates (0 when there
+// are fewer than k): k real documents score at least this, so it is a lower
+// bound of the final k-th key.
+__global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restrict__ cand,
+                                                         int64_t ntiles, int32_t P, int32_t k,
+                                                         uint64_t* __restrict__ theta) {
+  __shared__ uint64_t keys[kMergeP];
+  const int64_t q = blockIdx.x;
+  const int64_t nS = (ntiles + P - 1) / P;
+  topk_of(SrcSample{cand + q * ntiles * kTileM, P}, nS * kTileM, k, keys);
+  if (threadIdx.x == 0) theta[q] = keys[k - 1];
+}
 
 __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
     const uint64_t* __restrict__ cand, int64_t ntiles, int32_t k, int64_t maxflag,
@@ -486,22 +644,66 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
   return hipGetLastError();
 }
 
+static int env_mode() {
+  static const int mode = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
+  return mode;
+}
+
+// Sampling stride: every P-th tile is a sample tile; P is the largest of
+// {8, 4, 2} whose sample still yields >= 2k candidates (else one exact pass).
+static int sample_stride(int64_t ntiles, int k) {
+  static const bool off = getenv("BM25_NO_SAMPLE") != nullptr;
+  if (off) return 1;
+  for (int P = 8; P >= 2; P >>= 1) {
+    const int64_t nS = (ntiles + P - 1) / P;
+    if (ntiles >= 2 * P && nS * kTileM >= 2 * (int64_t)k) return P;
+  }
+  return 1;
+}
+
+template <int S, int PH>
+static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int P,
+                         const Workspace& ws, hipStream_t st) {
+  const int64_t nS = (ix.ntiles + P - 1) / P;
+  const int64_t nt = PH == kAll ? ix.ntiles : (PH == kSample ? nS : ix.ntiles - nS);
+  const int64_t grid = ((nt * Q + 7) >> 3) << 3;
+  if (grid == 0) return;
+  static const int rb = getenv("BM25_RB") ? atoi(getenv("BM25_RB")) : 8;
+  if (rb == 4)
+    hipLaunchKernelGGL((score_tiles_kernel<S, PH, 4>), dim3((unsigned)grid), dim3((1 << S) / kE),
+                       0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta,
+                       ws.cand, env_mode());
+  else if (rb == 12)
+    hipLaunchKernelGGL((score_tiles_kernel<S, PH, 12>), dim3((unsigned)grid), dim3((1 << S) / kE),
+                       0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta,
+                       ws.cand, env_mode());
+  else
+    hipLaunchKernelGGL((score_tiles_kernel<S, PH, 8>), dim3((unsigned)grid), dim3((1 << S) / kE),
+                       0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta,
+                       ws.cand, env_mode());
+}
+
 template <int S>
-static void launch_score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
+static void launch_score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
                            const Workspace& ws, hipStream_t st) {
-  const int64_t nitems = ix.ntiles * Q;
-  const int64_t grid = ((nitems + 7) >> 3) << 3;
-  hipLaunchKernelGGL(score_tiles_kernel<S>, dim3((unsigned)grid), dim3((1 << S) / kE), 0, st,
-                     args_of(ix), q, (int32_t)Q, (int32_t)T, ws.cand);
+  const int P = sample_stride(ix.ntiles, k);
+  if (P == 1) {
+    launch_phase<S, kAll>(ix, q, Q, T, 1, ws, st);
+    return;
+  }
+  launch_phase<S, kSample>(ix, q, Q, T, P, ws, st);
+  hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, ws.cand, ix.ntiles,
+                     (int32_t)P, (int32_t)k, ws.theta);
+  launch_phase<S, kRest>(ix, q, Q, T, P, ws, st);
 }
 
 hipError_t launch_score_tiles(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
-                              int64_t T, const Workspace& ws, hipStream_t stream) {
+                              int64_t T, int k, const Workspace& ws, hipStream_t stream) {
   if (Q == 0 || ix.ntiles == 0) return hipSuccess;
   switch (ix.tile_shift) {
-    case 13: launch_score_s<13>(ix, d_queries, Q, T, ws, stream); break;
-    case 14: launch_score_s<14>(ix, d_queries, Q, T, ws, stream); break;
-    case 15: launch_score_s<15>(ix, d_queries, Q, T, ws, stream); break;
+    case 13: launch_score_s<13>(ix, d_queries, Q, T, k, ws, stream); break;
+    case 14: launch_score_s<14>(ix, d_queries, Q, T, k, ws, stream); break;
+    case 15: launch_score_s<15>(ix, d_queries, Q, T, k, ws, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
