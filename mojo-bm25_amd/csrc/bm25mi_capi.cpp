@@ -85,6 +85,7 @@ void free_ws(Workspace& ws) {
   hipFree(ws.nflag);
   hipFree(ws.counters);
   hipFree(ws.queue);
+  hipFree(ws.wctr);
   ws = Workspace{};
 }
 
@@ -102,6 +103,7 @@ int ensure_ws(bm25_index* h, int64_t Q, int k) {
   HIP_TRY(hipMalloc(&ws.nflag, sizeof(int32_t) * q), "hipMalloc(nflag)");
   HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
   HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
+  HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * 16), "hipMalloc(wctr)");
   ws.cap_q = q;
   ws.cap_k = kk;
   return BM25_OK;

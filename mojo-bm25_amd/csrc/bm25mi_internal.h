@@ -69,6 +69,7 @@ struct Workspace {
   int32_t* nflag = nullptr;      // [Q]
   int32_t* counters = nullptr;   // [0] queue length, [1] queue pop cursor, [2..3] pad
   int32_t* queue = nullptr;      // [Q*maxflag] items = q*maxflag + i
+  int32_t* wctr = nullptr;       // [16] per-XCD-group item counters (2 score phases)
 };
 
 // Flag slots per query: a flagged tile holds kTileM keys of the top-(k-1), so

@@ -154,9 +154,15 @@ __device__ __forceinline__ void accumulate_tile(const IndexArgs& a, int64_t tile
           while (row >= sgpr(sm.rstart[s + 1])) ++s;
           const uint32_t rr = row - sgpr(sm.rstart[s]);
           const int64_t A0 = sgpr64(sm.abeg[s]) + (int64_t)rr * RW;
-          ld[b] = reinterpret_cast<const ushort4*>(a.ldoc + A0)[tid];
-          v[b] = reinterpret_cast<const float4*>(a.val + A0)[tid];
-          i0[b] = (int32_t)(rr * RW) + 4 * tid - (int32_t)sgpr(sm.off[s]);
+          // last 4-aligned group of the segment, relative to this row: lanes
+          // past it re-read that group (one cache line for all of them)
+          // instead of fetching postings of other terms
+          const uint32_t off = sgpr(sm.off[s]);
+          const uint32_t lastg = ((off + sgpr(sm.len[s]) - 1) & ~3u) - rr * RW;
+          const uint32_t g = min(4u * tid, lastg) >> 2;
+          ld[b] = reinterpret_cast<const ushort4*>(a.ldoc + A0)[g];
+          v[b] = reinterpret_cast<const float4*>(a.val + A0)[g];
+          i0[b] = (int32_t)(rr * RW) + 4 * tid - (int32_t)off;
           rs[b] = s;
         }
       }
@@ -366,6 +372,287 @@ __global__ __launch_bounds__((1 << S) / kE) void score_tiles_kernel(
   uint32_t key[kE];
   make_keys<S>(fv, tile, a.n_docs, key);
   select_tile<S>(key, tile, kTileM, out, sm);
+}
+
+// ---------------------------------------------------------------------------
+// Streaming (persistent) score kernel: the same per-item work as
+// score_tiles_kernel, software-pipelined across items so that memory latency
+// overlaps compute.  While item n is accumulated and selected, the first
+// posting rows of item n+1 are in flight (registers) and the segment
+// metadata of item n+2 (rel/indptr) is in flight; the query terms of item n+3
+// are loaded one iteration ahead of that.  Items are handed out in chunks
+// from one counter per XCD group (blockIdx % 8), in tile-major order, so the
+// workgroups of an XCD work on the same tile together (L2 reuse of the hot
+// posting segments across queries).  Requires T <= kTG.
+// ---------------------------------------------------------------------------
+struct ItemMeta {
+  int64_t abeg[kTG];
+  uint32_t off[kTG];
+  uint32_t len[kTG];
+  uint32_t rstart[kTG + 1];
+};
+
+constexpr int kFifo = 16;
+struct StreamShared {
+  ItemMeta meta[3];
+  int64_t fifo[kFifo];  // upcoming items of this workgroup
+  int32_t fhead, fcount, exhausted;
+  uint32_t red[2][16];
+  int32_t nsel[2];
+};
+
+template <int PH>
+__device__ __forceinline__ void item_tile(int64_t item, int64_t Q, int P, int64_t& tile,
+                                          int64_t& q) {
+  const int64_t ti = item / Q;
+  q = item - ti * Q;
+  if (PH == kAll) tile = ti;
+  else if (PH == kSample) tile = ti * P;
+  else tile = (ti / (P - 1)) * P + (ti % (P - 1)) + 1;
+}
+
+// Issue the segment-metadata loads of one query term (thread < T).
+struct MetaRegs {
+  uint32_t r0, r1;
+  int64_t ip;
+  bool ok;
+};
+__device__ __forceinline__ MetaRegs meta_issue(const IndexArgs& a, int32_t term, int64_t tile) {
+  MetaRegs m;
+  m.ok = term >= 0 && term < a.V;  // negative ids are padding (bm25_native.py:151)
+  const int64_t t = m.ok ? term : 0;
+  const uint32_t* r = a.rel + t * (a.ntiles + 1) + tile;
+  m.r0 = r[0];
+  m.r1 = r[1];
+  m.ip = a.indptr[t];
+  return m;
+}
+
+// Threads 0..T-1 (wave 0) publish their term's segment into `mt`: row counts
+// and their prefix via a wave scan (no block barrier needed inside).
+template <int S>
+__device__ __forceinline__ void meta_store(const MetaRegs& m, int T, ItemMeta& mt) {
+  constexpr uint32_t RW = 4 * ((1 << S) / kE);
+  const int tid = threadIdx.x;
+  uint32_t rows = 0;
+  if (tid < T) {
+    const int64_t lo = m.ip + m.r0;
+    const uint32_t len = m.ok ? m.r1 - m.r0 : 0u;
+    mt.abeg[tid] = lo & ~3ll;
+    mt.off[tid] = (uint32_t)(lo & 3);
+    mt.len[tid] = len;
+    rows = len ? (uint32_t)(((lo & 3) + len + RW - 1) / RW) : 0u;
+  }
+  if (tid < 64) {
+    uint32_t x = rows;
+#pragma unroll
+    for (int o = 1; o < kTG; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+      if ((tid & 63) >= o) x += y;
+    }
+    if (tid < T) mt.rstart[tid + 1] = x;
+    if (tid == 0) mt.rstart[0] = 0;
+  }
+}
+
+// Issue the loads of rows [row0, row0 + RB) of an item (block-uniform).
+// Every call issues exactly 2*RB loads, none under a branch (rows past the
+// item read a fixed in-bounds address and are marked rs = -1): the compiler's
+// vmcnt bookkeeping then stays exact across the software pipeline.
+template <int S, int RB>
+__device__ __forceinline__ void rows_issue(const IndexArgs& a, const ItemMeta& mt, int T,
+                                           uint32_t row0, ushort4 (&ld)[RB], float4 (&v)[RB],
+                                           int32_t (&i0)[RB], int (&rs)[RB]) {
+  constexpr uint32_t RW = 4 * ((1 << S) / kE);
+  const int tid = threadIdx.x;
+  const uint32_t R = sgpr(mt.rstart[T]);
+  int s = 0;
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    const uint32_t row = row0 + b;
+    int64_t A0 = 0;
+    uint32_t lastg = 0, rr = 0, off = 0;
+    rs[b] = -1;
+    if (row < R) {
+      while (row >= sgpr(mt.rstart[s + 1])) ++s;
+      rr = row - sgpr(mt.rstart[s]);
+      A0 = sgpr64(mt.abeg[s]) + (int64_t)rr * RW;
+      off = sgpr(mt.off[s]);
+      lastg = ((off + sgpr(mt.len[s]) - 1) & ~3u) - rr * RW;
+      rs[b] = s;
+    }
+    const uint32_t g = min(4u * tid, lastg) >> 2;
+    ld[b] = reinterpret_cast<const ushort4*>(a.ldoc + A0)[g];
+    v[b] = reinterpret_cast<const float4*>(a.val + A0)[g];
+    i0[b] = (int32_t)(rr * RW) + 4 * tid - (int32_t)off;
+  }
+}
+
+// Add a batch of rows (barrier between rows of different terms).
+template <int S, int RB>
+__device__ __forceinline__ void rows_add(const ItemMeta& mt, float* acc, const ushort4 (&ld)[RB],
+                                         const float4 (&v)[RB], const int32_t (&i0)[RB],
+                                         const int (&rs)[RB], int& last_s) {
+  constexpr int D = 1 << S;
+  const uint32_t dummy = D + (threadIdx.x & 63);
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    if (rs[b] < 0) break;
+    if (rs[b] != last_s) {
+      if (last_s >= 0) __syncthreads();  // previous term's adds complete
+      last_s = rs[b];
+    }
+    const uint32_t len = sgpr(mt.len[rs[b]]);
+    const uint32_t d0 = (uint32_t)(i0[b] + 0) < len ? (uint32_t)ld[b].x : dummy;
+    const uint32_t d1 = (uint32_t)(i0[b] + 1) < len ? (uint32_t)ld[b].y : dummy;
+    const uint32_t d2 = (uint32_t)(i0[b] + 2) < len ? (uint32_t)ld[b].z : dummy;
+    const uint32_t d3 = (uint32_t)(i0[b] + 3) < len ? (uint32_t)ld[b].w : dummy;
+    const float x0 = acc[d0], x1 = acc[d1], x2 = acc[d2], x3 = acc[d3];
+    acc[d0] = x0 + v[b].x;
+    acc[d1] = x1 + v[b].y;
+    acc[d2] = x2 + v[b].z;
+    acc[d3] = x3 + v[b].w;
+  }
+}
+
+__device__ __forceinline__ void fifo_refill(StreamShared& ss, int32_t* ctr, int64_t g_lo,
+                                            int64_t g_hi, int chunk) {
+  while (!ss.exhausted && ss.fcount + chunk <= kFifo) {
+    const int64_t c = g_lo + atomicAdd(ctr, chunk);
+    for (int i = 0; i < chunk; ++i) {
+      if (c + i >= g_hi) { ss.exhausted = 1; break; }
+      ss.fifo[(ss.fhead + ss.fcount) % kFifo] = c + i;
+      ++ss.fcount;
+    }
+  }
+}
+
+__device__ __forceinline__ int64_t fifo_peek(const StreamShared& ss, int j) {
+  return j < ss.fcount ? ss.fifo[(ss.fhead + j) % kFifo] : -1;
+}
+
+template <int S, int PH, int RB>
+__global__ __launch_bounds__((1 << S) / kE) void score_stream_kernel(
+    IndexArgs a, const int32_t* __restrict__ queries, int32_t Q, int32_t T, int32_t P,
+    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int32_t* __restrict__ wctr,
+    int32_t chunk) {
+  constexpr int D = 1 << S;
+  constexpr int NT = D / kE;
+  __shared__ __attribute__((aligned(16))) float acc[D + 64];
+  __shared__ StreamShared ss;
+  __shared__ TileShared sm;  // red / nsel of the selection helpers
+  const int tid = threadIdx.x;
+  const bool refiller = tid == NT - 64;  // lane 0 of the last wave grabs chunks
+  const int64_t nS = (a.ntiles + P - 1) / P;
+  const int64_t nt = PH == kAll ? a.ntiles : (PH == kSample ? nS : a.ntiles - nS);
+  const int64_t nitems = nt * Q;
+  const int64_t per = (nitems + 7) >> 3;
+  const int g = blockIdx.x & 7;
+  const int64_t g_lo = g * per, g_hi = min(nitems, g_lo + per);
+  int32_t* ctr = wctr + g;
+  const int tq = min(tid, T - 1);  // every thread loads a valid query slot
+
+  // ---- prologue: item list, zeroed accumulator, metadata of items 0 and 1
+  if (refiller) {
+    ss.fhead = 0;
+    ss.fcount = 0;
+    ss.exhausted = 0;
+    fifo_refill(ss, ctr, g_lo, g_hi, chunk);
+  }
+  float4* acc4 = reinterpret_cast<float4*>(acc);
+#pragma unroll
+  for (int j = 0; j < kE / 4; ++j) acc4[j * NT + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  const int64_t it0 = sgpr64(fifo_peek(ss, 0));
+  if (it0 < 0) return;  // block-uniform
+  int32_t qn;           // query term (thread tq) of the item two ahead
+  {
+    int64_t tile, q;
+    item_tile<PH>(it0, Q, P, tile, q);
+    const MetaRegs m0 = meta_issue(a, tid < T ? queries[q * T + tq] : -1, tile);
+    const int64_t it1 = sgpr64(fifo_peek(ss, 1));
+    item_tile<PH>(it1 >= 0 ? it1 : it0, Q, P, tile, q);
+    const MetaRegs m1 = meta_issue(a, tid < T ? queries[q * T + tq] : -1, tile);
+    const int64_t it2 = sgpr64(fifo_peek(ss, 2));
+    item_tile<PH>(it2 >= 0 ? it2 : it0, Q, P, tile, q);
+    qn = queries[q * T + tq];
+    meta_store<S>(m0, T, ss.meta[0]);
+    if (it1 >= 0) meta_store<S>(m1, T, ss.meta[1]);
+    if (tid == 0) sm.nsel = 0;
+  }
+  __syncthreads();
+  ushort4 ldA[RB], ldB[RB];
+  float4 vA[RB], vB[RB];
+  int32_t iA[RB], iB[RB];
+  int rsA[RB], rsB[RB];
+  rows_issue<S, RB>(a, ss.meta[0], T, 0, ldA, vA, iA, rsA);
+
+  // One pipeline step: item n's first rows are in (ld, v, i, rs); item n+1's
+  // first rows are issued into (ldN, ...).  Returns false after the last item.
+  auto step = [&](int n, ushort4 (&ld)[RB], float4 (&v)[RB], int32_t (&i0)[RB], int (&rs)[RB],
+                  ushort4 (&ldN)[RB], float4 (&vN)[RB], int32_t (&iN)[RB],
+                  int (&rsN)[RB]) -> bool {
+    const int64_t it = sgpr64(fifo_peek(ss, 0));
+    const int64_t nx = sgpr64(fifo_peek(ss, 1));
+    const int64_t n2 = sgpr64(fifo_peek(ss, 2));
+    const int64_t n3 = sgpr64(fifo_peek(ss, 3));
+    const ItemMeta& mc = ss.meta[n % 3];
+    int64_t tile, q;
+    item_tile<PH>(it, Q, P, tile, q);
+    // (a) metadata of item n+2, query terms of item n+3 (fixed load count)
+    int64_t t2, q2;
+    item_tile<PH>(n2 >= 0 ? n2 : it, Q, P, t2, q2);
+    const MetaRegs m2 = meta_issue(a, tid < T ? qn : -1, t2);
+    item_tile<PH>(n3 >= 0 ? n3 : it, Q, P, t2, q2);
+    qn = queries[q2 * T + tq];
+    // (b) first rows of item n+1 (without a next item the loads still go out,
+    //     from the current item's valid segments, and are never used)
+    rows_issue<S, RB>(a, nx >= 0 ? ss.meta[(n + 1) % 3] : mc, T, 0, ldN, vN, iN, rsN);
+    // (c) accumulate item n: prefetched rows, then any further rows
+    int last_s = -1;
+    rows_add<S, RB>(mc, acc, ld, v, i0, rs, last_s);
+    const uint32_t R = sgpr(mc.rstart[T]);
+    for (uint32_t rb = RB; rb < R; rb += RB) {
+      ushort4 ldX[RB];
+      float4 vX[RB];
+      int32_t iX[RB];
+      int rsX[RB];
+      rows_issue<S, RB>(a, mc, T, rb, ldX, vX, iX, rsX);
+      rows_add<S, RB>(mc, acc, ldX, vX, iX, rsX, last_s);
+    }
+    __syncthreads();
+    // (d) selection of item n; the entries are zeroed for item n+1 as read
+    {
+      float fv[kE];
+      load_entries<S>(acc, fv);
+#pragma unroll
+      for (int j = 0; j < kE / 4; ++j) acc4[j * NT + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+      uint64_t* out = cand + (q * a.ntiles + tile) * kTileM;
+      bool exact = true;
+      if (PH == kRest) exact = emit_above<S>(fv, tile, a.n_docs, theta[q], out, sm) > kTileM;
+      if (exact) {
+        uint32_t key[kE];
+        make_keys<S>(fv, tile, a.n_docs, key);
+        select_tile<S>(key, tile, kTileM, out, sm);
+      }
+    }
+    __syncthreads();  // every read of sm.nsel / red and of meta[n % 3] is done
+    // (e) publish item n+2's metadata, advance the item list
+    if (n2 >= 0) meta_store<S>(m2, T, ss.meta[(n + 2) % 3]);
+    if (tid == 0) sm.nsel = 0;
+    if (refiller) {
+      ss.fhead = (ss.fhead + 1) % kFifo;
+      --ss.fcount;
+      fifo_refill(ss, ctr, g_lo, g_hi, chunk);
+    }
+    __syncthreads();
+    return nx >= 0;
+  };
+
+  for (int n = 0;; n += 2) {
+    if (!step(n, ldA, vA, iA, rsA, ldB, vB, iB, rsB)) break;
+    if (!step(n + 1, ldB, vB, iB, rsB, ldA, vA, iA, rsA)) break;
+  }
 }
 
 // Exact top-k of each flagged tile; persistent, pulls items from the queue
@@ -661,6 +948,31 @@ static int sample_stride(int64_t ntiles, int k) {
   return 1;
 }
 
+template <int S, int PH, int RB>
+static void launch_stream(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int P,
+                          const Workspace& ws, int32_t* wctr, hipStream_t st) {
+  static int grid = 0;
+  if (grid == 0) {
+    int dev = 0, cus = 0, occ = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, score_stream_kernel<S, PH, RB>,
+                                                 (1 << S) / kE, 0);
+    const char* e = getenv("BM25_STREAM_WG_PER_CU");
+    if (e) occ = atoi(e);
+    grid = ((cus * (occ > 0 ? occ : 1) + 7) / 8) * 8;
+    if (grid < 8) grid = 8;
+  }
+  hipLaunchKernelGGL((score_stream_kernel<S, PH, RB>), dim3((unsigned)grid), dim3((1 << S) / kE),
+                     0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta, ws.cand,
+                     wctr, (int32_t)8);
+}
+
+static bool use_stream(int64_t T) {
+  static const bool off = getenv("BM25_NO_STREAM") != nullptr;
+  return !off && T >= 1 && T <= kTG;
+}
+
 template <int S, int PH>
 static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int P,
                          const Workspace& ws, hipStream_t st) {
@@ -668,13 +980,13 @@ static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t Q, int64_
   const int64_t nt = PH == kAll ? ix.ntiles : (PH == kSample ? nS : ix.ntiles - nS);
   const int64_t grid = ((nt * Q + 7) >> 3) << 3;
   if (grid == 0) return;
+  if (use_stream(T)) {
+    launch_stream<S, PH, 4>(ix, q, Q, T, P, ws, ws.wctr + (PH == kRest ? 8 : 0), st);
+    return;
+  }
   static const int rb = getenv("BM25_RB") ? atoi(getenv("BM25_RB")) : 8;
   if (rb == 4)
     hipLaunchKernelGGL((score_tiles_kernel<S, PH, 4>), dim3((unsigned)grid), dim3((1 << S) / kE),
-                       0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta,
-                       ws.cand, env_mode());
-  else if (rb == 12)
-    hipLaunchKernelGGL((score_tiles_kernel<S, PH, 12>), dim3((unsigned)grid), dim3((1 << S) / kE),
                        0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta,
                        ws.cand, env_mode());
   else
@@ -700,6 +1012,10 @@ static void launch_score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int6
 hipError_t launch_score_tiles(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
                               int64_t T, int k, const Workspace& ws, hipStream_t stream) {
   if (Q == 0 || ix.ntiles == 0) return hipSuccess;
+  if (use_stream(T)) {
+    const hipError_t e = hipMemsetAsync(ws.wctr, 0, 16 * sizeof(int32_t), stream);
+    if (e != hipSuccess) return e;
+  }
   switch (ix.tile_shift) {
     case 13: launch_score_s<13>(ix, d_queries, Q, T, k, ws, stream); break;
     case 14: launch_score_s<14>(ix, d_queries, Q, T, k, ws, stream); break;
