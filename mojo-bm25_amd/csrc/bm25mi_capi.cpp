@@ -85,16 +85,31 @@ void free_ws(Workspace& ws) {
   hipFree(ws.nflag);
   hipFree(ws.counters);
   hipFree(ws.queue);
+  hipFree(ws.desc);
   hipFree(ws.wctr);
+  hipFree(ws.ovq);
   ws = Workspace{};
 }
 
-int ensure_ws(bm25_index* h, int64_t Q, int k) {
+int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   Workspace& ws = h->ws;
+  const int64_t nd = (T >= 1 && T <= kDescMaxT) ? h->ix.ntiles * Q * T : 0;
+  if (nd > ws.cap_desc) {
+    hipFree(ws.desc);
+    ws.desc = nullptr;
+    ws.cap_desc = 0;
+    HIP_TRY(hipMalloc(&ws.desc, sizeof(SegDesc) * nd), "hipMalloc(desc)");
+    ws.cap_desc = nd;
+  }
   if (Q <= ws.cap_q && k <= ws.cap_k) return BM25_OK;
   const int64_t q = std::max(Q, ws.cap_q);
   const int64_t kk = std::max<int64_t>(k, ws.cap_k);
+  SegDesc* keep_desc = ws.desc;
+  const int64_t keep_cap = ws.cap_desc;
+  ws.desc = nullptr;
   free_ws(ws);
+  ws.desc = keep_desc;
+  ws.cap_desc = keep_cap;
   const int64_t mf = maxflag_for((int)kk, h->ix.ntiles);
   HIP_TRY(hipMalloc(&ws.cand, sizeof(uint64_t) * q * h->ix.ntiles * kTileM), "hipMalloc(cand)");
   HIP_TRY(hipMalloc(&ws.theta, sizeof(uint64_t) * q), "hipMalloc(theta)");
@@ -104,6 +119,7 @@ int ensure_ws(bm25_index* h, int64_t Q, int k) {
   HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
   HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
   HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * 16), "hipMalloc(wctr)");
+  HIP_TRY(hipMalloc(&ws.ovq, sizeof(int32_t) * q * h->ix.ntiles), "hipMalloc(ovq)");
   ws.cap_q = q;
   ws.cap_k = kk;
   return BM25_OK;
@@ -161,7 +177,7 @@ EventPair* next_events(bm25_index* h) {
 int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, int k,
                int32_t* d_docs, float* d_scores, hipStream_t st) {
   if (Q == 0 || k == 0) return BM25_OK;
-  int rc = ensure_ws(h, Q, k);
+  int rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   EventPair* ev = next_events(h);
   if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
@@ -224,8 +240,8 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     if (ip[t + 1] - ip[t] > n_docs)
       return fail(BM25_EINVAL, "column %lld has more entries than n_docs", (long long)t);
   }
-  int shift = env_int("BM25_TILE_SHIFT", 14);
-  if (!tile_shift_supported(shift)) return fail(BM25_EINVAL, "BM25_TILE_SHIFT=%d not compiled (13,14,15)", shift);
+  int shift = env_int("BM25_TILE_SHIFT", 13);
+  if (!tile_shift_supported(shift)) return fail(BM25_EINVAL, "BM25_TILE_SHIFT=%d not compiled (12..15)", shift);
   const int64_t ntiles = (n_docs + (1LL << shift) - 1) >> shift;
   if (ntiles > 65536) return fail(BM25_EINVAL, "n_docs=%lld needs %lld tiles (> 65536)", (long long)n_docs, (long long)ntiles);
 

@@ -60,6 +60,15 @@ struct DevIndex {
   float* val = nullptr;
 };
 
+// Segment descriptor of one (item, query term): the term's postings inside
+// the item's tile are [beg, beg + len); pre = postings of the item's earlier
+// terms (the term's offset in the item's concatenated posting stream).
+struct SegDesc {
+  int64_t beg;
+  uint32_t len;
+  uint32_t pre;
+};
+
 struct Workspace {
   int64_t cap_q = 0, cap_k = 0;
   uint64_t* cand = nullptr;      // [Q][ntiles][kTileM]
@@ -67,8 +76,12 @@ struct Workspace {
   uint64_t* cand2 = nullptr;     // [Q][maxflag][k]  exact top-k of re-scored tiles
   int32_t* flag_tiles = nullptr; // [Q][maxflag]
   int32_t* nflag = nullptr;      // [Q]
-  int32_t* counters = nullptr;   // [0] queue length, [1] queue pop cursor, [2..3] pad
+  int32_t* counters = nullptr;   // [0]/[1] rescore queue length / pop cursor,
+                                 // [2]/[3] overflow queue length / pop cursor
+  int32_t* ovq = nullptr;        // [Q*ntiles] REST tiles to fix up (q*ntiles + tile)
   int32_t* queue = nullptr;      // [Q*maxflag] items = q*maxflag + i
+  SegDesc* desc = nullptr;       // [ntiles][Q][T] when T <= 16
+  int64_t cap_desc = 0;
   int32_t* wctr = nullptr;       // [16] per-XCD-group item counters (2 score phases)
 };
 
@@ -96,6 +109,8 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,
 hipError_t launch_score_tiles(const DevIndex& ix, const int32_t* d_queries,
                               int64_t Q, int64_t T, int k, const Workspace& ws,
                               hipStream_t stream);
+// Queries with at most this many terms use per-batch segment descriptors.
+constexpr int kDescMaxT = 16;
 // Merge + rescore + final merge.
 hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries,
                          int64_t Q, int64_t T, int k, const Workspace& ws,

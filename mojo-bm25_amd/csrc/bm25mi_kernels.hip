@@ -36,6 +36,10 @@ constexpr int kE = 32;   // accumulator entries owned by a thread in selection
 
 enum Phase { kAll = 0, kSample = 1, kRest = 2 };
 
+// Candidate-slot marker of a REST tile with >= kTileM keys above theta (never
+// a real key: that would be a NaN score at doc 0).
+constexpr uint64_t kOverflowKey = ~0ull;
+
 struct IndexArgs {
   const int64_t* indptr;
   const uint32_t* rel;
@@ -63,6 +67,15 @@ __device__ __forceinline__ uint32_t sgpr(uint32_t v) {
 }
 __device__ __forceinline__ int64_t sgpr64(int64_t v) {
   const uint32_t lo = sgpr((uint32_t)v), hi = sgpr((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Value of lane `l` (block-uniform l) of a VGPR, as a scalar.
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ int64_t lane_i64(int64_t v, int l) {
+  const uint32_t lo = lane_u32((uint32_t)v, l), hi = lane_u32((uint32_t)((uint64_t)v >> 32), l);
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
@@ -96,7 +109,8 @@ template <int S, int kRB = 4>
 __device__ __forceinline__ void accumulate_tile(const IndexArgs& a, int64_t tile,
                                                 const int32_t* __restrict__ qterms,
                                                 int T, float* acc, TileShared& sm,
-                                                int mode = 0) {
+                                                int mode = 0,
+                                                const SegDesc* __restrict__ dsc = nullptr) {
   constexpr int D = 1 << S;
   constexpr int NT = D / kE;
   constexpr uint32_t RW = 4 * NT;  // postings per row
@@ -112,6 +126,27 @@ __device__ __forceinline__ void accumulate_tile(const IndexArgs& a, int64_t tile
 
   for (int g0 = 0; g0 < T; g0 += kTG) {
     const int ng = min(kTG, T - g0);
+    if (dsc) {  // segments precomputed for the batch (desc_kernel): one load level
+      if (tid < 64) {
+        uint32_t rows = 0;
+        if (tid < ng) {
+          const SegDesc d = dsc[tid];
+          sm.abeg[tid] = d.beg & ~3ll;
+          sm.off[tid] = (uint32_t)(d.beg & 3);
+          sm.len[tid] = d.len;
+          rows = d.len ? (uint32_t)(((d.beg & 3) + d.len + RW - 1) / RW) : 0u;
+        }
+        uint32_t x = rows;  // inclusive scan of row counts over the wave
+#pragma unroll
+        for (int o = 1; o < kTG; o <<= 1) {
+          const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+          if (tid >= o) x += y;
+        }
+        if (tid < ng) sm.rstart[tid + 1] = x;
+        if (tid == 0) sm.rstart[0] = 0;
+      }
+      __syncthreads();
+    } else {
     __syncthreads();  // zeroing / previous group's reads of sm are done
     if (tid < ng) {
       const int32_t term = qterms[g0 + tid];
@@ -138,7 +173,14 @@ __device__ __forceinline__ void accumulate_tile(const IndexArgs& a, int64_t tile
       }
     }
     __syncthreads();
-    const uint32_t R = (mode & 4) ? 0u : sgpr(sm.rstart[ng]);
+    }
+    // Per-term metadata into VGPR lanes (lane s holds term s): uniform values
+    // are then v_readlane'd, with no LDS round trip on the address path.
+    const int li = min(tid & 63, kTG - 1);
+    const int64_t m_abeg = sm.abeg[li];
+    const uint32_t m_off = sm.off[li], m_len = sm.len[li];
+    const uint32_t m_rs0 = sm.rstart[li], m_rs1 = sm.rstart[li + 1];
+    const uint32_t R = (mode & 4) ? 0u : lane_u32(m_rs1, ng - 1);
     int s = 0;          // term of the current row (block-uniform)
     int last_s = -1;    // term of the last added row
     for (uint32_t rb = 0; rb < R; rb += kRB) {
@@ -151,14 +193,14 @@ __device__ __forceinline__ void accumulate_tile(const IndexArgs& a, int64_t tile
         const uint32_t row = rb + b;
         rs[b] = -1;
         if (row < R) {
-          while (row >= sgpr(sm.rstart[s + 1])) ++s;
-          const uint32_t rr = row - sgpr(sm.rstart[s]);
-          const int64_t A0 = sgpr64(sm.abeg[s]) + (int64_t)rr * RW;
+          while (row >= lane_u32(m_rs1, s)) ++s;
+          const uint32_t rr = row - lane_u32(m_rs0, s);
+          const int64_t A0 = lane_i64(m_abeg, s) + (int64_t)rr * RW;
           // last 4-aligned group of the segment, relative to this row: lanes
           // past it re-read that group (one cache line for all of them)
           // instead of fetching postings of other terms
-          const uint32_t off = sgpr(sm.off[s]);
-          const uint32_t lastg = ((off + sgpr(sm.len[s]) - 1) & ~3u) - rr * RW;
+          const uint32_t off = lane_u32(m_off, s);
+          const uint32_t lastg = ((off + lane_u32(m_len, s) - 1) & ~3u) - rr * RW;
           const uint32_t g = min(4u * tid, lastg) >> 2;
           ld[b] = reinterpret_cast<const ushort4*>(a.ldoc + A0)[g];
           v[b] = reinterpret_cast<const float4*>(a.val + A0)[g];
@@ -179,7 +221,7 @@ __device__ __forceinline__ void accumulate_tile(const IndexArgs& a, int64_t tile
           if (last_s >= 0) __syncthreads();  // previous term's adds complete
           last_s = rs[b];
         }
-        const uint32_t len = sgpr(sm.len[rs[b]]);
+        const uint32_t len = lane_u32(m_len, rs[b]);
         const uint32_t d0 = (uint32_t)(i0[b] + 0) < len ? (uint32_t)ld[b].x : dummy;
         const uint32_t d1 = (uint32_t)(i0[b] + 1) < len ? (uint32_t)ld[b].y : dummy;
         const uint32_t d2 = (uint32_t)(i0[b] + 2) < len ? (uint32_t)ld[b].z : dummy;
@@ -277,55 +319,51 @@ __device__ __forceinline__ void select_tile(uint32_t (&key)[kE], int64_t tile, i
   }
 }
 
-// Threshold emission (REST tiles): write the keys > theta (at most kTileM;
-// slots past the count are zeroed) and return the block-wide count; above
-// kTileM the caller runs the exact selection instead.  The test runs on the
-// fp32 sums directly (one compare per entry); only a lane holding theta's
-// exact score compares doc ids.  Accumulators are never -0.0 (a sum that
-// starts at +0.0 cannot produce it) and docs past n_docs hold 0.0, which can
-// only pass when theta's score is negative — those are masked explicitly.
+// Threshold emission (REST tiles), barrier-free: the keys > theta go to the
+// tile's candidate slots (pre-zeroed for the search) through an LDS slot
+// counter.  With at most kTileM - 1 keys above theta the tile is complete
+// (its last slot stays empty, so the merge never flags it).  With more, the
+// lane that holds the kTileM-th key appends the tile to the overflow queue,
+// and fixup_kernel rewrites its slots with the tile's exact top-kTileM.  The
+// test runs on the fp32 sums (one compare per entry, after a max early-out);
+// only a lane holding theta's exact score compares doc ids.  Accumulators are
+// never -0.0 (a sum that starts at +0.0 cannot produce it) and docs past
+// n_docs hold 0.0, which can only pass when theta's score is negative: those
+// are masked explicitly.
 template <int S>
-__device__ __forceinline__ int emit_above(const float (&fv)[kE], int64_t tile, int64_t n_docs,
-                                          uint64_t theta, uint64_t* __restrict__ out,
-                                          TileShared& sm) {
+__device__ __forceinline__ void emit_above(const float (&fv)[kE], int64_t tile, int64_t n_docs,
+                                           uint64_t theta, uint64_t* __restrict__ out,
+                                           TileShared& sm, int32_t* ovq, int32_t* ovn,
+                                           int32_t code) {
   constexpr int D = 1 << S;
   const int tid = threadIdx.x;
   const float th = key_score((uint32_t)(theta >> 32));
   const uint32_t th_doc = 0xFFFFFFFFu - (uint32_t)theta;
   const int64_t doc0 = tile * D + (int64_t)tid * kE;
   const int64_t lim_hi = n_docs - doc0;  // entries e >= lim_hi are past n_docs
+  float mx = fv[0];
+#pragma unroll
+  for (int e = 1; e < kE; ++e) mx = fmaxf(mx, fv[e]);
+  if (mx < th && lim_hi >= kE) return;  // common: nothing of this lane passes
+  const int64_t lim_tie = (int64_t)th_doc - doc0;  // ties pass for e < lim_tie
   int c = 0;
-  bool tie = false;
+#pragma unroll
+  for (int e = 0; e < kE; ++e)
+    c += (e < lim_hi) & ((fv[e] > th) | ((fv[e] == th) & (e < lim_tie)));
+  if (c == 0) return;
+  int pos = atomicAdd(&sm.nsel, c);
+  const int first = pos;
 #pragma unroll
   for (int e = 0; e < kE; ++e) {
-    c += fv[e] > th;
-    tie |= fv[e] == th;
-  }
-  if (tie || lim_hi < kE) {  // rare: exact per-entry rule
-    const int64_t lim_tie = (int64_t)th_doc - doc0;  // ties pass for e < lim_tie
-    c = 0;
-#pragma unroll
-    for (int e = 0; e < kE; ++e)
-      c += (e < lim_hi) & ((fv[e] > th) | ((fv[e] == th) & (e < lim_tie)));
-  }
-  if (c > 0) {
-    const int64_t lim_tie = (int64_t)th_doc - doc0;
-    int pos = atomicAdd(&sm.nsel, c);
-#pragma unroll
-    for (int e = 0; e < kE; ++e) {
-      const bool pass = (e < lim_hi) & ((fv[e] > th) | ((fv[e] == th) & (e < lim_tie)));
-      if (pass) {
-        if (pos < kTileM)
-          out[pos] = ((uint64_t)score_key(fv[e]) << 32) |
-                     (uint64_t)(0xFFFFFFFFu - (uint32_t)(doc0 + e));
-        ++pos;
-      }
+    const bool pass = (e < lim_hi) & ((fv[e] > th) | ((fv[e] == th) & (e < lim_tie)));
+    if (pass) {
+      if (pos < kTileM - 1)
+        out[pos] = ((uint64_t)score_key(fv[e]) << 32) |
+                   (uint64_t)(0xFFFFFFFFu - (uint32_t)(doc0 + e));
+      ++pos;
     }
   }
-  __syncthreads();
-  const int n = sm.nsel;
-  if (n < kTileM && tid < kTileM - n) out[n + tid] = 0;
-  return n;
+  if (first <= kTileM - 1 && pos > kTileM - 1) ovq[atomicAdd(ovn, 1)] = code;  // one lane
 }
 
 // Work item -> (tile, query).  Blocks are dealt round-robin over the 8 XCDs
@@ -353,12 +391,15 @@ __device__ __forceinline__ bool item_of(int64_t ntiles, int64_t Q, int P, int64_
 template <int S, int PH, int RB>
 __global__ __launch_bounds__((1 << S) / kE) void score_tiles_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t Q, int32_t T, int32_t P,
-    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int mode) {
+    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand,
+    const SegDesc* __restrict__ desc, int32_t* __restrict__ ovq, int32_t* __restrict__ ovn,
+    int mode) {
   __shared__ __attribute__((aligned(16))) float acc[(1 << S) + 64];
   __shared__ TileShared sm;
   int64_t tile, q;
   if (!item_of<PH>(a.ntiles, Q, P, tile, q)) return;
-  accumulate_tile<S, RB>(a, tile, queries + q * T, T, acc, sm, mode);
+  accumulate_tile<S, RB>(a, tile, queries + q * T, T, acc, sm, mode,
+                         desc ? desc + (tile * Q + q) * T : nullptr);
   uint64_t* out = cand + (q * a.ntiles + tile) * kTileM;
   if (mode & 1) {  // ablation: no selection
     if (threadIdx.x == 0) out[0] = __float_as_uint(acc[0]);
@@ -367,7 +408,9 @@ __global__ __launch_bounds__((1 << S) / kE) void score_tiles_kernel(
   float fv[kE];
   load_entries<S>(acc, fv);
   if (PH == kRest) {
-    if (emit_above<S>(fv, tile, a.n_docs, theta[q], out, sm) <= kTileM) return;
+    emit_above<S>(fv, tile, a.n_docs, theta[q], out, sm, ovq, ovn,
+                  (int32_t)(q * a.ntiles + tile));
+    return;
   }
   uint32_t key[kE];
   make_keys<S>(fv, tile, a.n_docs, key);
@@ -375,30 +418,32 @@ __global__ __launch_bounds__((1 << S) / kE) void score_tiles_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Streaming (persistent) score kernel: the same per-item work as
-// score_tiles_kernel, software-pipelined across items so that memory latency
-// overlaps compute.  While item n is accumulated and selected, the first
-// posting rows of item n+1 are in flight (registers) and the segment
-// metadata of item n+2 (rel/indptr) is in flight; the query terms of item n+3
-// are loaded one iteration ahead of that.  Items are handed out in chunks
-// from one counter per XCD group (blockIdx % 8), in tile-major order, so the
-// workgroups of an XCD work on the same tile together (L2 reuse of the hot
-// posting segments across queries).  Requires T <= kTG.
+// Pipelined score kernel (persistent).  An item's postings are read as one
+// concatenated stream (term after term, positions 0..total); thread t holds
+// positions t + NT*j, j < J ("slots", 2 VGPRs each: LDS slot | term << 16,
+// and the score).  While item n is accumulated and selected, the slots of
+// item n+1 are in flight and the segment descriptors of item n+2 (from
+// desc_kernel) are in flight, so an item's memory latency overlaps the
+// previous item's compute.  Items come in chunks from one counter per XCD
+// group (blockIdx % 8) in tile-major order: the workgroups of an XCD share a
+// tile (L2 reuse of its hot posting segments across queries).  Every
+// pipeline step issues a fixed number of global loads, none under a branch,
+// and the two slot register sets alternate by unrolling (no copies), so the
+// compiler's vmcnt waits stay counted instead of draining the pipeline.
+// Requires 1 <= T <= kTG.
 // ---------------------------------------------------------------------------
-struct ItemMeta {
-  int64_t abeg[kTG];
-  uint32_t off[kTG];
-  uint32_t len[kTG];
-  uint32_t rstart[kTG + 1];
+constexpr int kFifo = 16;
+constexpr uint32_t kNoTerm = 31u;
+
+struct PipeMeta {
+  int64_t delta[kTG];       // global posting index - stream position, per term
+  uint32_t start[kTG + 1];  // stream position of each term's first posting; [T] = total
 };
 
-constexpr int kFifo = 16;
-struct StreamShared {
-  ItemMeta meta[3];
+struct PipeShared {
+  PipeMeta meta[3];
   int64_t fifo[kFifo];  // upcoming items of this workgroup
   int32_t fhead, fcount, exhausted;
-  uint32_t red[2][16];
-  int32_t nsel[2];
 };
 
 template <int PH>
@@ -411,135 +456,126 @@ __device__ __forceinline__ void item_tile(int64_t item, int64_t Q, int P, int64_
   else tile = (ti / (P - 1)) * P + (ti % (P - 1)) + 1;
 }
 
-// Issue the segment-metadata loads of one query term (thread < T).
-struct MetaRegs {
-  uint32_t r0, r1;
-  int64_t ip;
-  bool ok;
-};
-__device__ __forceinline__ MetaRegs meta_issue(const IndexArgs& a, int32_t term, int64_t tile) {
-  MetaRegs m;
-  m.ok = term >= 0 && term < a.V;  // negative ids are padding (bm25_native.py:151)
-  const int64_t t = m.ok ? term : 0;
-  const uint32_t* r = a.rel + t * (a.ntiles + 1) + tile;
-  m.r0 = r[0];
-  m.r1 = r[1];
-  m.ip = a.indptr[t];
-  return m;
-}
-
-// Threads 0..T-1 (wave 0) publish their term's segment into `mt`: row counts
-// and their prefix via a wave scan (no block barrier needed inside).
-template <int S>
-__device__ __forceinline__ void meta_store(const MetaRegs& m, int T, ItemMeta& mt) {
-  constexpr uint32_t RW = 4 * ((1 << S) / kE);
-  const int tid = threadIdx.x;
-  uint32_t rows = 0;
-  if (tid < T) {
-    const int64_t lo = m.ip + m.r0;
-    const uint32_t len = m.ok ? m.r1 - m.r0 : 0u;
-    mt.abeg[tid] = lo & ~3ll;
-    mt.off[tid] = (uint32_t)(lo & 3);
-    mt.len[tid] = len;
-    rows = len ? (uint32_t)(((lo & 3) + len + RW - 1) / RW) : 0u;
-  }
-  if (tid < 64) {
-    uint32_t x = rows;
-#pragma unroll
-    for (int o = 1; o < kTG; o <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-      if ((tid & 63) >= o) x += y;
-    }
-    if (tid < T) mt.rstart[tid + 1] = x;
-    if (tid == 0) mt.rstart[0] = 0;
-  }
-}
-
-// Issue the loads of rows [row0, row0 + RB) of an item (block-uniform).
-// Every call issues exactly 2*RB loads, none under a branch (rows past the
-// item read a fixed in-bounds address and are marked rs = -1): the compiler's
-// vmcnt bookkeeping then stays exact across the software pipeline.
-template <int S, int RB>
-__device__ __forceinline__ void rows_issue(const IndexArgs& a, const ItemMeta& mt, int T,
-                                           uint32_t row0, ushort4 (&ld)[RB], float4 (&v)[RB],
-                                           int32_t (&i0)[RB], int (&rs)[RB]) {
-  constexpr uint32_t RW = 4 * ((1 << S) / kE);
-  const int tid = threadIdx.x;
-  const uint32_t R = sgpr(mt.rstart[T]);
-  int s = 0;
-#pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    const uint32_t row = row0 + b;
-    int64_t A0 = 0;
-    uint32_t lastg = 0, rr = 0, off = 0;
-    rs[b] = -1;
-    if (row < R) {
-      while (row >= sgpr(mt.rstart[s + 1])) ++s;
-      rr = row - sgpr(mt.rstart[s]);
-      A0 = sgpr64(mt.abeg[s]) + (int64_t)rr * RW;
-      off = sgpr(mt.off[s]);
-      lastg = ((off + sgpr(mt.len[s]) - 1) & ~3u) - rr * RW;
-      rs[b] = s;
-    }
-    const uint32_t g = min(4u * tid, lastg) >> 2;
-    ld[b] = reinterpret_cast<const ushort4*>(a.ldoc + A0)[g];
-    v[b] = reinterpret_cast<const float4*>(a.val + A0)[g];
-    i0[b] = (int32_t)(rr * RW) + 4 * tid - (int32_t)off;
-  }
-}
-
-// Add a batch of rows (barrier between rows of different terms).
-template <int S, int RB>
-__device__ __forceinline__ void rows_add(const ItemMeta& mt, float* acc, const ushort4 (&ld)[RB],
-                                         const float4 (&v)[RB], const int32_t (&i0)[RB],
-                                         const int (&rs)[RB], int& last_s) {
-  constexpr int D = 1 << S;
-  const uint32_t dummy = D + (threadIdx.x & 63);
-#pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    if (rs[b] < 0) break;
-    if (rs[b] != last_s) {
-      if (last_s >= 0) __syncthreads();  // previous term's adds complete
-      last_s = rs[b];
-    }
-    const uint32_t len = sgpr(mt.len[rs[b]]);
-    const uint32_t d0 = (uint32_t)(i0[b] + 0) < len ? (uint32_t)ld[b].x : dummy;
-    const uint32_t d1 = (uint32_t)(i0[b] + 1) < len ? (uint32_t)ld[b].y : dummy;
-    const uint32_t d2 = (uint32_t)(i0[b] + 2) < len ? (uint32_t)ld[b].z : dummy;
-    const uint32_t d3 = (uint32_t)(i0[b] + 3) < len ? (uint32_t)ld[b].w : dummy;
-    const float x0 = acc[d0], x1 = acc[d1], x2 = acc[d2], x3 = acc[d3];
-    acc[d0] = x0 + v[b].x;
-    acc[d1] = x1 + v[b].y;
-    acc[d2] = x2 + v[b].z;
-    acc[d3] = x3 + v[b].w;
-  }
-}
-
-__device__ __forceinline__ void fifo_refill(StreamShared& ss, int32_t* ctr, int64_t g_lo,
+__device__ __forceinline__ void fifo_refill(PipeShared& ps, int32_t* ctr, int64_t g_lo,
                                             int64_t g_hi, int chunk) {
-  while (!ss.exhausted && ss.fcount + chunk <= kFifo) {
+  while (!ps.exhausted && ps.fcount + chunk <= kFifo) {
     const int64_t c = g_lo + atomicAdd(ctr, chunk);
     for (int i = 0; i < chunk; ++i) {
-      if (c + i >= g_hi) { ss.exhausted = 1; break; }
-      ss.fifo[(ss.fhead + ss.fcount) % kFifo] = c + i;
-      ++ss.fcount;
+      if (c + i >= g_hi) { ps.exhausted = 1; break; }
+      ps.fifo[(ps.fhead + ps.fcount) % kFifo] = c + i;
+      ++ps.fcount;
     }
   }
 }
 
-__device__ __forceinline__ int64_t fifo_peek(const StreamShared& ss, int j) {
-  return j < ss.fcount ? ss.fifo[(ss.fhead + j) % kFifo] : -1;
+__device__ __forceinline__ int64_t fifo_peek(const PipeShared& ps, int j) {
+  return j < ps.fcount ? ps.fifo[(ps.fhead + j) % kFifo] : -1;
 }
 
-template <int S, int PH, int RB>
-__global__ __launch_bounds__((1 << S) / kE) void score_stream_kernel(
+// Descriptor registers of one term (thread < T) -> the stage's PipeMeta.
+__device__ __forceinline__ void meta_put(const SegDesc& d, int T, PipeMeta& m) {
+  const int tid = threadIdx.x;
+  if (tid < T) {
+    m.delta[tid] = d.beg - (int64_t)d.pre;
+    m.start[tid] = d.pre;
+    if (tid == T - 1) m.start[T] = d.pre + d.len;
+  }
+}
+
+// The stage's per-term metadata in VGPR lanes (lane s = term s): uniform
+// values are v_readlane'd on the address path instead of read from LDS.
+struct MetaLanes {
+  int64_t delta;
+  uint32_t start, start1;  // start[s], start[s + 1]
+  uint32_t total;
+};
+__device__ __forceinline__ MetaLanes meta_lanes(const PipeMeta& m, int T) {
+  const int li = min((int)(threadIdx.x & 63), kTG - 1);
+  MetaLanes r;
+  r.delta = m.delta[li];
+  r.start = m.start[li];
+  r.start1 = m.start[li + 1];
+  r.total = sgpr(m.start[T]);
+  return r;
+}
+
+// Issue the J slot loads of stream positions [p0 + NT*j + t].  Exactly 2*J
+// loads per call, unconditionally (positions past the stream re-read the
+// row's first posting and are tagged kNoTerm).
+template <int S, int J>
+__device__ __forceinline__ void slots_issue(const IndexArgs& a, const MetaLanes& ml, int T,
+                                            uint32_t p0, uint32_t (&lt)[J], float (&v)[J]) {
+  constexpr uint32_t NT = (1u << S) / kE;
+  const uint32_t tid = threadIdx.x;
+  int s = 0;  // term of the current slot-row's first position (block-uniform)
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t r0 = p0 + NT * j;
+    uint32_t P = r0 + tid;
+    uint32_t st = kNoTerm;
+    int64_t delta = 0;
+    if (r0 < ml.total) {
+      while (s + 1 < T && lane_u32(ml.start1, s) <= r0) ++s;
+      st = s;
+      delta = lane_i64(ml.delta, s);
+      const uint32_t rend = min(r0 + NT, ml.total);
+      for (int sl = s + 1; sl < T && lane_u32(ml.start, sl) < rend; ++sl) {
+        if (P >= lane_u32(ml.start, sl)) {
+          st = sl;
+          delta = lane_i64(ml.delta, sl);
+        }
+      }
+      if (P >= ml.total) {  // past the stream: reload row position r0 (term s)
+        P = r0;
+        st = kNoTerm;
+        delta = lane_i64(ml.delta, s);
+      }
+    } else {
+      P = 0;
+    }
+    const int64_t g = (int64_t)P + delta;
+    lt[j] = (uint32_t)a.ldoc[g] | (st << 16);
+    v[j] = a.val[g];
+  }
+}
+
+// Add the slots of stream positions [p0, p0 + NT*J) in term order.
+template <int S, int J>
+__device__ __forceinline__ void slots_add(const MetaLanes& ml, int T, uint32_t p0, float* acc,
+                                          const uint32_t (&lt)[J], const float (&v)[J],
+                                          int& last_s) {
+  constexpr uint32_t NT = (1u << S) / kE;
+  const uint32_t dummy = (1u << S) + (threadIdx.x & 63);
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t r0 = p0 + NT * j;
+    if (r0 >= ml.total) break;
+    while (s + 1 < T && lane_u32(ml.start1, s) <= r0) ++s;
+    const uint32_t rend = min(r0 + NT, ml.total);
+    for (int sc = s; sc < T && lane_u32(ml.start, sc) < rend; ++sc) {
+      if (lane_u32(ml.start1, sc) == lane_u32(ml.start, sc)) continue;  // empty term
+      if (sc != last_s) {
+        if (last_s >= 0) __syncthreads();  // previous term's adds complete
+        last_s = sc;
+      }
+      const uint32_t d = (lt[j] >> 16) == (uint32_t)sc ? (lt[j] & 0xFFFFu) : dummy;
+      const float x = acc[d];
+      acc[d] = x + v[j];
+    }
+  }
+}
+
+template <int S, int PH, int J>
+__global__ __launch_bounds__((1 << S) / kE, 4) void score_pipe_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t Q, int32_t T, int32_t P,
-    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int32_t* __restrict__ wctr,
-    int32_t chunk) {
+    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand,
+    const SegDesc* __restrict__ desc, int32_t* __restrict__ wctr, int32_t chunk,
+    int32_t* __restrict__ ovq, int32_t* __restrict__ ovn) {
   constexpr int D = 1 << S;
   constexpr int NT = D / kE;
   __shared__ __attribute__((aligned(16))) float acc[D + 64];
-  __shared__ StreamShared ss;
+  __shared__ PipeShared ps;
   __shared__ TileShared sm;  // red / nsel of the selection helpers
   const int tid = threadIdx.x;
   const bool refiller = tid == NT - 64;  // lane 0 of the last wave grabs chunks
@@ -550,108 +586,168 @@ __global__ __launch_bounds__((1 << S) / kE) void score_stream_kernel(
   const int g = blockIdx.x & 7;
   const int64_t g_lo = g * per, g_hi = min(nitems, g_lo + per);
   int32_t* ctr = wctr + g;
-  const int tq = min(tid, T - 1);  // every thread loads a valid query slot
+  const int td = min(tid, T - 1);  // every thread loads a valid descriptor slot
 
-  // ---- prologue: item list, zeroed accumulator, metadata of items 0 and 1
   if (refiller) {
-    ss.fhead = 0;
-    ss.fcount = 0;
-    ss.exhausted = 0;
-    fifo_refill(ss, ctr, g_lo, g_hi, chunk);
+    ps.fhead = 0;
+    ps.fcount = 0;
+    ps.exhausted = 0;
+    fifo_refill(ps, ctr, g_lo, g_hi, chunk);
   }
+  if (tid == 0) sm.nsel = 0;
   float4* acc4 = reinterpret_cast<float4*>(acc);
 #pragma unroll
   for (int j = 0; j < kE / 4; ++j) acc4[j * NT + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  const int64_t it0 = sgpr64(fifo_peek(ss, 0));
+  const int64_t it0 = sgpr64(fifo_peek(ps, 0));
   if (it0 < 0) return;  // block-uniform
-  int32_t qn;           // query term (thread tq) of the item two ahead
   {
     int64_t tile, q;
     item_tile<PH>(it0, Q, P, tile, q);
-    const MetaRegs m0 = meta_issue(a, tid < T ? queries[q * T + tq] : -1, tile);
-    const int64_t it1 = sgpr64(fifo_peek(ss, 1));
+    const SegDesc d0 = desc[(tile * Q + q) * T + td];
+    const int64_t it1 = sgpr64(fifo_peek(ps, 1));
     item_tile<PH>(it1 >= 0 ? it1 : it0, Q, P, tile, q);
-    const MetaRegs m1 = meta_issue(a, tid < T ? queries[q * T + tq] : -1, tile);
-    const int64_t it2 = sgpr64(fifo_peek(ss, 2));
-    item_tile<PH>(it2 >= 0 ? it2 : it0, Q, P, tile, q);
-    qn = queries[q * T + tq];
-    meta_store<S>(m0, T, ss.meta[0]);
-    if (it1 >= 0) meta_store<S>(m1, T, ss.meta[1]);
-    if (tid == 0) sm.nsel = 0;
+    const SegDesc d1 = desc[(tile * Q + q) * T + td];
+    meta_put(d0, T, ps.meta[0]);
+    meta_put(d1, T, ps.meta[1]);
   }
   __syncthreads();
-  ushort4 ldA[RB], ldB[RB];
-  float4 vA[RB], vB[RB];
-  int32_t iA[RB], iB[RB];
-  int rsA[RB], rsB[RB];
-  rows_issue<S, RB>(a, ss.meta[0], T, 0, ldA, vA, iA, rsA);
+  uint32_t ltA[J], ltB[J];
+  float vA[J], vB[J];
+  slots_issue<S, J>(a, meta_lanes(ps.meta[0], T), T, 0, ltA, vA);
 
-  // One pipeline step: item n's first rows are in (ld, v, i, rs); item n+1's
-  // first rows are issued into (ldN, ...).  Returns false after the last item.
-  auto step = [&](int n, ushort4 (&ld)[RB], float4 (&v)[RB], int32_t (&i0)[RB], int (&rs)[RB],
-                  ushort4 (&ldN)[RB], float4 (&vN)[RB], int32_t (&iN)[RB],
-                  int (&rsN)[RB]) -> bool {
-    const int64_t it = sgpr64(fifo_peek(ss, 0));
-    const int64_t nx = sgpr64(fifo_peek(ss, 1));
-    const int64_t n2 = sgpr64(fifo_peek(ss, 2));
-    const int64_t n3 = sgpr64(fifo_peek(ss, 3));
-    const ItemMeta& mc = ss.meta[n % 3];
-    int64_t tile, q;
+  auto step = [&](int n, uint32_t (&lt)[J], float (&v)[J], uint32_t (&ltN)[J],
+                  float (&vN)[J]) -> bool {
+    const int64_t it = sgpr64(fifo_peek(ps, 0));
+    const int64_t nx = sgpr64(fifo_peek(ps, 1));
+    const int64_t n2 = sgpr64(fifo_peek(ps, 2));
+    const PipeMeta& mc = ps.meta[n % 3];
+    int64_t tile, q, t2, q2;
     item_tile<PH>(it, Q, P, tile, q);
-    // (a) metadata of item n+2, query terms of item n+3 (fixed load count)
-    int64_t t2, q2;
+    // (a) descriptors of item n+2
     item_tile<PH>(n2 >= 0 ? n2 : it, Q, P, t2, q2);
-    const MetaRegs m2 = meta_issue(a, tid < T ? qn : -1, t2);
-    item_tile<PH>(n3 >= 0 ? n3 : it, Q, P, t2, q2);
-    qn = queries[q2 * T + tq];
-    // (b) first rows of item n+1 (without a next item the loads still go out,
-    //     from the current item's valid segments, and are never used)
-    rows_issue<S, RB>(a, nx >= 0 ? ss.meta[(n + 1) % 3] : mc, T, 0, ldN, vN, iN, rsN);
-    // (c) accumulate item n: prefetched rows, then any further rows
+    const SegDesc d2 = desc[(t2 * Q + q2) * T + td];
+    const MetaLanes mlc = meta_lanes(mc, T);
+    // (b) slots of item n+1 (without a next item: harmless reloads of item n)
+    slots_issue<S, J>(a, nx >= 0 ? meta_lanes(ps.meta[(n + 1) % 3], T) : mlc, T, 0, ltN, vN);
+    // (c) accumulate item n: prefetched slots, then the rest of its stream
     int last_s = -1;
-    rows_add<S, RB>(mc, acc, ld, v, i0, rs, last_s);
-    const uint32_t R = sgpr(mc.rstart[T]);
-    for (uint32_t rb = RB; rb < R; rb += RB) {
-      ushort4 ldX[RB];
-      float4 vX[RB];
-      int32_t iX[RB];
-      int rsX[RB];
-      rows_issue<S, RB>(a, mc, T, rb, ldX, vX, iX, rsX);
-      rows_add<S, RB>(mc, acc, ldX, vX, iX, rsX, last_s);
+    slots_add<S, J>(mlc, T, 0, acc, lt, v, last_s);
+    for (uint32_t p0 = NT * J; p0 < mlc.total; p0 += NT * J) {
+      uint32_t ltX[J];
+      float vX[J];
+      slots_issue<S, J>(a, mlc, T, p0, ltX, vX);
+      slots_add<S, J>(mlc, T, p0, acc, ltX, vX, last_s);
     }
     __syncthreads();
-    // (d) selection of item n; the entries are zeroed for item n+1 as read
+    // (d) selection of item n; entries are zeroed for item n+1 as they are read
     {
       float fv[kE];
       load_entries<S>(acc, fv);
 #pragma unroll
       for (int j = 0; j < kE / 4; ++j) acc4[j * NT + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
       uint64_t* out = cand + (q * a.ntiles + tile) * kTileM;
-      bool exact = true;
-      if (PH == kRest) exact = emit_above<S>(fv, tile, a.n_docs, theta[q], out, sm) > kTileM;
-      if (exact) {
+      if (PH == kRest) {
+        emit_above<S>(fv, tile, a.n_docs, theta[q], out, sm, ovq, ovn,
+                      (int32_t)(q * a.ntiles + tile));
+      } else {
         uint32_t key[kE];
         make_keys<S>(fv, tile, a.n_docs, key);
         select_tile<S>(key, tile, kTileM, out, sm);
       }
     }
-    __syncthreads();  // every read of sm.nsel / red and of meta[n % 3] is done
-    // (e) publish item n+2's metadata, advance the item list
-    if (n2 >= 0) meta_store<S>(m2, T, ss.meta[(n + 2) % 3]);
+    __syncthreads();  // reads of sm.nsel / red and of meta[n % 3] are done
+    // (e) publish item n+2's descriptors, advance the item list
+    if (n2 >= 0) meta_put(d2, T, ps.meta[(n + 2) % 3]);
     if (tid == 0) sm.nsel = 0;
     if (refiller) {
-      ss.fhead = (ss.fhead + 1) % kFifo;
-      --ss.fcount;
-      fifo_refill(ss, ctr, g_lo, g_hi, chunk);
+      ps.fhead = (ps.fhead + 1) % kFifo;
+      --ps.fcount;
+      fifo_refill(ps, ctr, g_lo, g_hi, chunk);
     }
     __syncthreads();
     return nx >= 0;
   };
 
   for (int n = 0;; n += 2) {
-    if (!step(n, ldA, vA, iA, rsA, ldB, vB, iB, rsB)) break;
-    if (!step(n + 1, ldB, vB, iB, rsB, ldA, vA, iA, rsA)) break;
+    if (!step(n, ltA, vA, ltB, vB)) break;
+    if (!step(n + 1, ltB, vB, ltA, vA)) break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Slot score kernel: one workgroup per (tile, query) like score_tiles_kernel,
+// but the item's postings are read as one dense concatenated stream (thread t
+// takes positions t + NT*j): every lane of a load carries a posting, each
+// load is 2 + 4 bytes per lane, and the RMW touches one posting per lane per
+// slot-row, instead of 4-wide rows of which ~3/4 of the lanes idle on short
+// segments.  Needs the batch's segment descriptors (1 <= T <= kTG).
+// ---------------------------------------------------------------------------
+template <int S, int PH, int J>
+__global__ __launch_bounds__((1 << S) / kE) void score_slots_kernel(
+    IndexArgs a, int32_t Q, int32_t T, int32_t P, const uint64_t* __restrict__ theta,
+    uint64_t* __restrict__ cand, const SegDesc* __restrict__ desc, int32_t* __restrict__ ovq,
+    int32_t* __restrict__ ovn) {
+  constexpr int D = 1 << S;
+  constexpr int NT = D / kE;
+  __shared__ __attribute__((aligned(16))) float acc[D + 64];
+  __shared__ PipeMeta pm;
+  __shared__ TileShared sm;
+  const int tid = threadIdx.x;
+  int64_t tile, q;
+  if (!item_of<PH>(a.ntiles, Q, P, tile, q)) return;
+  float4* acc4 = reinterpret_cast<float4*>(acc);
+#pragma unroll
+  for (int j = 0; j < kE / 4; ++j) acc4[j * NT + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (tid == 0) sm.nsel = 0;
+  if (tid < T) meta_put(desc[(tile * Q + q) * T + tid], T, pm);
+  __syncthreads();
+  const MetaLanes ml = meta_lanes(pm, T);
+  int last_s = -1;
+  for (uint32_t p0 = 0; p0 < ml.total; p0 += NT * J) {
+    uint32_t lt[J];
+    float v[J];
+    slots_issue<S, J>(a, ml, T, p0, lt, v);
+    slots_add<S, J>(ml, T, p0, acc, lt, v, last_s);
+  }
+  __syncthreads();
+  float fv[kE];
+  load_entries<S>(acc, fv);
+  uint64_t* out = cand + (q * a.ntiles + tile) * kTileM;
+  if (PH == kRest) {
+    emit_above<S>(fv, tile, a.n_docs, theta[q], out, sm, ovq, ovn,
+                  (int32_t)(q * a.ntiles + tile));
+    return;
+  }
+  uint32_t key[kE];
+  make_keys<S>(fv, tile, a.n_docs, key);
+  select_tile<S>(key, tile, kTileM, out, sm);
+}
+
+// Segment descriptors of every (tile, query, term) of the batch, tile-major
+// like the score kernels' items: one thread per (tile, query).
+template <int S>
+__global__ __launch_bounds__(256) void desc_kernel(IndexArgs a, const int32_t* __restrict__ queries,
+                                                   int32_t Q, int32_t T,
+                                                   SegDesc* __restrict__ desc) {
+  constexpr uint32_t RW = 4 * ((1 << S) / kE);
+  const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= a.ntiles * Q) return;
+  const int64_t tile = item / Q, q = item - tile * Q;
+  uint32_t pre = 0;
+  (void)RW;
+  for (int s = 0; s < T; ++s) {
+    const int32_t term = queries[q * T + s];
+    int64_t beg = 0;
+    uint32_t len = 0;
+    if (term >= 0 && term < a.V) {  // negative ids are padding (bm25_native.py:151)
+      const uint32_t* r = a.rel + (int64_t)term * (a.ntiles + 1) + tile;
+      const uint32_t r0 = r[0], r1 = r[1];
+      beg = a.indptr[term] + r0;
+      len = r1 - r0;
+    }
+    desc[item * T + s] = SegDesc{beg, len, pre};
+    pre += len;
   }
 }
 
@@ -679,6 +775,32 @@ __global__ __launch_bounds__((1 << S) / kE) void rescore_kernel(
     uint32_t key[kE];
     make_keys<S>(fv, tile, a.n_docs, key);
     select_tile<S>(key, tile, k, ws.cand2 + (int64_t)code * k, sm);
+  }
+}
+
+// Exact top-kTileM of the REST tiles that overflowed the threshold pass;
+// persistent, queue-driven like rescore_kernel.
+template <int S>
+__global__ __launch_bounds__((1 << S) / kE) void fixup_kernel(
+    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, uint64_t* __restrict__ cand,
+    const int32_t* __restrict__ ovq, int32_t* __restrict__ counters) {
+  __shared__ __attribute__((aligned(16))) float acc[(1 << S) + 64];
+  __shared__ TileShared sm;
+  const int32_t n_items = counters[2];
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) sm.item = atomicAdd(&counters[3], 1);
+    __syncthreads();
+    const int32_t it = sm.item;
+    if (it >= n_items) break;
+    const int32_t code = ovq[it];
+    const int64_t q = code / a.ntiles, tile = code - q * a.ntiles;
+    accumulate_tile<S>(a, tile, queries + q * T, T, acc, sm);
+    float fv[kE];
+    load_entries<S>(acc, fv);
+    uint32_t key[kE];
+    make_keys<S>(fv, tile, a.n_docs, key);
+    select_tile<S>(key, tile, kTileM, cand + (int64_t)code * kTileM, sm);
   }
 }
 
@@ -790,6 +912,42 @@ __device__ void topk_of(const Src& src, int64_t n_total, int k, uint64_t* keys) 
   }
 }
 
+// Same result as topk_of when at least k candidates are >= lo: candidates
+// below lo (or empty) are dropped while compacting into LDS (wave ballots, one
+// LDS atomic per wave), so only the survivors are sorted.
+template <class Src>
+__device__ void topk_compact(const Src& src, int64_t n_total, int k, uint64_t lo, uint64_t* keys,
+                             int* cnt) {
+  const int B = next_pow2(k);
+  if (threadIdx.x == 0) *cnt = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t rounds = (n_total + blockDim.x - 1) / blockDim.x;
+  for (int64_t r = 0; r < rounds; ++r) {
+    const int64_t i = r * blockDim.x + threadIdx.x;
+    const uint64_t key = i < n_total ? src(i) : 0ull;
+    const bool keep = key != 0ull && key != kOverflowKey && key >= lo;
+    const unsigned long long m = __ballot(keep);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(cnt, (int)__popcll(m));
+    base = __shfl(base, 0, 64);
+    const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (keep && pos < kMergeP) keys[pos] = key;
+  }
+  __syncthreads();
+  const int c = *cnt;
+  if (c > kMergeP) {  // too many survivors: full chunked sort
+    __syncthreads();
+    topk_of(src, n_total, k, keys);
+    return;
+  }
+  const int n = next_pow2(c > B ? c : B);
+  for (int i = c + threadIdx.x; i < n; i += blockDim.x) keys[i] = 0ull;
+  __syncthreads();
+  bitonic_sort_desc(keys, n);
+}
+
 __device__ __forceinline__ void write_result(const uint64_t* keys, int k, int64_t row,
                                              int64_t doc_offset, int32_t* __restrict__ docs,
                                              float* __restrict__ scores) {
@@ -854,13 +1012,16 @@ __global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restr
 
 __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
     const uint64_t* __restrict__ cand, int64_t ntiles, int32_t k, int64_t maxflag,
-    int64_t doc_offset, Workspace ws, int32_t* __restrict__ docs, float* __restrict__ scores) {
+    int64_t doc_offset, Workspace ws, const uint64_t* __restrict__ theta_s,
+    int32_t* __restrict__ docs, float* __restrict__ scores) {
   __shared__ uint64_t keys[kMergeP];
-  __shared__ int32_t s_nflag;
+  __shared__ int32_t s_nflag, s_cnt;
   const int64_t q = blockIdx.x;
   const uint64_t* c = cand + q * ntiles * kTileM;
   if (threadIdx.x == 0) s_nflag = 0;
-  topk_of(SrcFirst{c}, ntiles * kTileM, k, keys);
+  // theta_s (sampling pass): k sample candidates are >= it, so nothing below
+  // it can reach the top-k
+  topk_compact(SrcFirst{c}, ntiles * kTileM, k, theta_s ? theta_s[q] : 0ull, keys, &s_cnt);
   const uint64_t theta = keys[k - 1];
   if (k > kTileM) {
     // A tile whose kTileM-th candidate beats theta may hold unreported docs
@@ -918,7 +1079,7 @@ __global__ __launch_bounds__(kMergeNT) void merge_lists_kernel(
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-bool tile_shift_supported(int s) { return s == 13 || s == 14 || s == 15; }
+bool tile_shift_supported(int s) { return s >= 12 && s <= 15; }
 
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int32_t* d_err,
                                hipStream_t stream) {
@@ -939,8 +1100,7 @@ static int env_mode() {
 // Sampling stride: every P-th tile is a sample tile; P is the largest of
 // {8, 4, 2} whose sample still yields >= 2k candidates (else one exact pass).
 static int sample_stride(int64_t ntiles, int k) {
-  static const bool off = getenv("BM25_NO_SAMPLE") != nullptr;
-  if (off) return 1;
+  if (getenv("BM25_NO_SAMPLE")) return 1;
   for (int P = 8; P >= 2; P >>= 1) {
     const int64_t nS = (ntiles + P - 1) / P;
     if (ntiles >= 2 * P && nS * kTileM >= 2 * (int64_t)k) return P;
@@ -948,29 +1108,39 @@ static int sample_stride(int64_t ntiles, int k) {
   return 1;
 }
 
-template <int S, int PH, int RB>
-static void launch_stream(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int P,
-                          const Workspace& ws, int32_t* wctr, hipStream_t st) {
+static bool use_desc(int64_t T) {
+  return !getenv("BM25_NO_DESC") && T >= 1 && T <= kDescMaxT;
+}
+
+// The pipelined kernel is opt-in (BM25_PIPE=1): on config 3 it is still
+// slower than the per-item kernel (measurements).
+static bool use_pipe(int64_t T) {
+  return getenv("BM25_PIPE") && use_desc(T) && T <= kTG;
+}
+
+template <int S, int PH>
+static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int P,
+                        const Workspace& ws, hipStream_t st) {
+  constexpr int J = 8;
   static int grid = 0;
   if (grid == 0) {
     int dev = 0, cus = 0, occ = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, score_stream_kernel<S, PH, RB>,
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, score_pipe_kernel<S, PH, J>,
                                                  (1 << S) / kE, 0);
-    const char* e = getenv("BM25_STREAM_WG_PER_CU");
+    const char* e = getenv("BM25_PIPE_WG_PER_CU");
     if (e) occ = atoi(e);
     grid = ((cus * (occ > 0 ? occ : 1) + 7) / 8) * 8;
-    if (grid < 8) grid = 8;
   }
-  hipLaunchKernelGGL((score_stream_kernel<S, PH, RB>), dim3((unsigned)grid), dim3((1 << S) / kE),
-                     0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta, ws.cand,
-                     wctr, (int32_t)8);
+  hipLaunchKernelGGL((score_pipe_kernel<S, PH, J>), dim3((unsigned)grid), dim3((1 << S) / kE), 0,
+                     st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta, ws.cand,
+                     ws.desc, ws.wctr + (PH == kRest ? 8 : 0), (int32_t)8, ws.ovq,
+                     ws.counters + 2);
 }
 
-static bool use_stream(int64_t T) {
-  static const bool off = getenv("BM25_NO_STREAM") != nullptr;
-  return !off && T >= 1 && T <= kTG;
+static bool use_slots(int64_t T) {
+  return getenv("BM25_SLOTS") && use_desc(T) && T <= kTG;
 }
 
 template <int S, int PH>
@@ -980,24 +1150,46 @@ static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t Q, int64_
   const int64_t nt = PH == kAll ? ix.ntiles : (PH == kSample ? nS : ix.ntiles - nS);
   const int64_t grid = ((nt * Q + 7) >> 3) << 3;
   if (grid == 0) return;
-  if (use_stream(T)) {
-    launch_stream<S, PH, 4>(ix, q, Q, T, P, ws, ws.wctr + (PH == kRest ? 8 : 0), st);
+  if (use_pipe(T)) {
+    launch_pipe<S, PH>(ix, q, Q, T, P, ws, st);
     return;
   }
-  static const int rb = getenv("BM25_RB") ? atoi(getenv("BM25_RB")) : 8;
+  if (use_slots(T)) {
+    const int J = getenv("BM25_J") ? atoi(getenv("BM25_J")) : 8;
+    if (J == 16)
+      hipLaunchKernelGGL((score_slots_kernel<S, PH, 16>), dim3((unsigned)grid),
+                         dim3((1 << S) / kE), 0, st, args_of(ix), (int32_t)Q, (int32_t)T,
+                         (int32_t)P, ws.theta, ws.cand, ws.desc, ws.ovq, ws.counters + 2);
+    else
+      hipLaunchKernelGGL((score_slots_kernel<S, PH, 8>), dim3((unsigned)grid),
+                         dim3((1 << S) / kE), 0, st, args_of(ix), (int32_t)Q, (int32_t)T,
+                         (int32_t)P, ws.theta, ws.cand, ws.desc, ws.ovq, ws.counters + 2);
+    return;
+  }
+  const int rb = getenv("BM25_RB") ? atoi(getenv("BM25_RB")) : 8;
   if (rb == 4)
     hipLaunchKernelGGL((score_tiles_kernel<S, PH, 4>), dim3((unsigned)grid), dim3((1 << S) / kE),
                        0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta,
-                       ws.cand, env_mode());
+                       ws.cand, use_desc(T) ? ws.desc : nullptr, ws.ovq, ws.counters + 2,
+                       env_mode());
   else
     hipLaunchKernelGGL((score_tiles_kernel<S, PH, 8>), dim3((unsigned)grid), dim3((1 << S) / kE),
                        0, st, args_of(ix), q, (int32_t)Q, (int32_t)T, (int32_t)P, ws.theta,
-                       ws.cand, env_mode());
+                       ws.cand, use_desc(T) ? ws.desc : nullptr, ws.ovq, ws.counters + 2,
+                       env_mode());
 }
 
 template <int S>
 static void launch_score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
                            const Workspace& ws, hipStream_t st) {
+  if (use_pipe(T)) hipMemsetAsync(ws.wctr, 0, 16 * sizeof(int32_t), st);
+  hipMemsetAsync(ws.counters, 0, 4 * sizeof(int32_t), st);
+  hipMemsetAsync(ws.cand, 0, sizeof(uint64_t) * Q * ix.ntiles * kTileM, st);
+  if (use_desc(T)) {
+    const int64_t n = ix.ntiles * Q;
+    hipLaunchKernelGGL(desc_kernel<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       args_of(ix), q, (int32_t)Q, (int32_t)T, ws.desc);
+  }
   const int P = sample_stride(ix.ntiles, k);
   if (P == 1) {
     launch_phase<S, kAll>(ix, q, Q, T, 1, ws, st);
@@ -1007,16 +1199,16 @@ static void launch_score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int6
   hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, ws.cand, ix.ntiles,
                      (int32_t)P, (int32_t)k, ws.theta);
   launch_phase<S, kRest>(ix, q, Q, T, P, ws, st);
+  hipLaunchKernelGGL(fixup_kernel<S>, dim3(256), dim3((1 << S) / kE), 0, st, args_of(ix), q,
+                     (int32_t)T, ws.cand, ws.ovq, ws.counters);
 }
 
 hipError_t launch_score_tiles(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
                               int64_t T, int k, const Workspace& ws, hipStream_t stream) {
   if (Q == 0 || ix.ntiles == 0) return hipSuccess;
-  if (use_stream(T)) {
-    const hipError_t e = hipMemsetAsync(ws.wctr, 0, 16 * sizeof(int32_t), stream);
-    if (e != hipSuccess) return e;
-  }
+
   switch (ix.tile_shift) {
+    case 12: launch_score_s<12>(ix, d_queries, Q, T, k, ws, stream); break;
     case 13: launch_score_s<13>(ix, d_queries, Q, T, k, ws, stream); break;
     case 14: launch_score_s<14>(ix, d_queries, Q, T, k, ws, stream); break;
     case 15: launch_score_s<15>(ix, d_queries, Q, T, k, ws, stream); break;
@@ -1037,12 +1229,15 @@ hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries, int64_t Q
                          hipStream_t stream) {
   if (Q == 0 || k == 0) return hipSuccess;
   const int64_t maxflag = maxflag_for(k, ix.ntiles);
-  hipError_t e = hipMemsetAsync(ws.counters, 0, 4 * sizeof(int32_t), stream);
+  hipError_t e = hipMemsetAsync(ws.counters, 0, 2 * sizeof(int32_t), stream);
   if (e != hipSuccess) return e;
+  const bool sampled = sample_stride(ix.ntiles, k) > 1;
   hipLaunchKernelGGL(merge_first_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, stream, ws.cand,
-                     ix.ntiles, (int32_t)k, maxflag, ix.doc_offset, ws, d_docs, d_scores);
+                     ix.ntiles, (int32_t)k, maxflag, ix.doc_offset, ws,
+                     sampled ? ws.theta : nullptr, d_docs, d_scores);
   if (k > kTileM) {
     switch (ix.tile_shift) {
+      case 12: launch_rescore_s<12>(ix, d_queries, T, k, maxflag, ws, stream); break;
       case 13: launch_rescore_s<13>(ix, d_queries, T, k, maxflag, ws, stream); break;
       case 14: launch_rescore_s<14>(ix, d_queries, T, k, maxflag, ws, stream); break;
       case 15: launch_rescore_s<15>(ix, d_queries, T, k, maxflag, ws, stream); break;
@@ -1060,6 +1255,7 @@ hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query, int64
   if (ix.ntiles == 0) return hipSuccess;
   const dim3 grid((unsigned)ix.ntiles);
   switch (ix.tile_shift) {
+    case 12: hipLaunchKernelGGL(scores_dense_kernel<12>, grid, dim3((1 << 12) / kE), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
     case 13: hipLaunchKernelGGL(scores_dense_kernel<13>, grid, dim3((1 << 13) / kE), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
     case 14: hipLaunchKernelGGL(scores_dense_kernel<14>, grid, dim3((1 << 14) / kE), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
     case 15: hipLaunchKernelGGL(scores_dense_kernel<15>, grid, dim3((1 << 15) / kE), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
