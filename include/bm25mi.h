@@ -128,14 +128,23 @@ int bm25_merge_topk_device(int device, const int32_t* d_docs,
                            void* stream);
 
 /*
- * Kernel timing of the dominant kernel (score_tiles), measured with HIP
- * events recorded on the search stream around every launch while enabled.
+ * Timing of the score pass (sample + theta + rest score kernels, the HBM
+ * bound part of a search), measured with HIP events recorded on the search
+ * stream around it in every search while enabled.
  * bm25_profile_enable(idx, 1) resets the accumulators.
  */
 int bm25_profile_enable(bm25_index* idx, int on);
 int bm25_profile_read(bm25_index* idx, double* score_ms_total,
                       int64_t* score_launches, double* total_ms,
                       int64_t* searches, int64_t* rescored_tiles);
+
+/*
+ * Selection statistics of the last search on the handle (diagnostics; waits
+ * for the device): tiles whose exact top-k had to be recomputed, and queries
+ * that took the exact fallback stage (candidate list overflow).
+ */
+int bm25_search_stats(bm25_index* idx, int64_t* rescored_tiles,
+                      int64_t* fallback_queries);
 
 #ifdef __cplusplus
 }

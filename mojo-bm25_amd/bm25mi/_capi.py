@@ -58,6 +58,7 @@ _SIGS = {
                                ctypes.c_int),
     "bm25_profile_enable": ([_P, ctypes.c_int], ctypes.c_int),
     "bm25_profile_read": ([_P, _PD, _PI64, _PD, _PI64, _PI64], ctypes.c_int),
+    "bm25_search_stats": ([_P, _PI64, _PI64], ctypes.c_int),
 }
 for _name, (_args, _res) in _SIGS.items():
     _f = getattr(lib, _name)

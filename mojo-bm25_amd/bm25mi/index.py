@@ -133,6 +133,14 @@ class GpuIndex:
         return {"score_ms": sm.value, "score_launches": sl.value, "total_ms": tm.value,
                 "searches": ns.value, "rescored_tiles_last": rs.value}
 
+    def search_stats(self) -> dict:
+        """Selection statistics of the last search: tiles re-scored exactly,
+        queries sent to the exact fallback stage."""
+        r = ctypes.c_int64()
+        f = ctypes.c_int64()
+        check(lib.bm25_search_stats(self._h, ctypes.byref(r), ctypes.byref(f)))
+        return {"rescored_tiles": r.value, "fallback_queries": f.value}
+
 
 def merge_topk_device(device: int, d_docs, d_scores, W: int, Q: int, k: int, d_out_docs,
                       d_out_scores, stream=None) -> None:

@@ -80,46 +80,48 @@ namespace {
 void free_ws(Workspace& ws) {
   hipFree(ws.cand);
   hipFree(ws.theta);
+  hipFree(ws.list);
+  hipFree(ws.list_cnt);
+  hipFree(ws.fb);
   hipFree(ws.cand2);
   hipFree(ws.flag_tiles);
   hipFree(ws.nflag);
-  hipFree(ws.counters);
   hipFree(ws.queue);
-  hipFree(ws.desc);
-  hipFree(ws.wctr);
-  hipFree(ws.ovq);
+  hipFree(ws.counters);
   ws = Workspace{};
 }
 
+// Candidate-list capacity per query: the keys above theta of the non-sample
+// tiles number about (P-1)*k; a list that overflows sends its query to the
+// exact fallback stage (BM25_LIST_CAP overrides, for tests).
+int32_t list_cap_for(int64_t k) {
+  const int e = env_int("BM25_LIST_CAP", 0);
+  if (e > 0) return e;
+  return (int32_t)std::min<int64_t>(65536, std::max<int64_t>(2048, 64 * k));
+}
+
 int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
+  (void)T;
   Workspace& ws = h->ws;
-  const int64_t nd = (T >= 1 && T <= kDescMaxT) ? h->ix.ntiles * Q * T : 0;
-  if (nd > ws.cap_desc) {
-    hipFree(ws.desc);
-    ws.desc = nullptr;
-    ws.cap_desc = 0;
-    HIP_TRY(hipMalloc(&ws.desc, sizeof(SegDesc) * nd), "hipMalloc(desc)");
-    ws.cap_desc = nd;
-  }
   if (Q <= ws.cap_q && k <= ws.cap_k) return BM25_OK;
   const int64_t q = std::max(Q, ws.cap_q);
   const int64_t kk = std::max<int64_t>(k, ws.cap_k);
-  SegDesc* keep_desc = ws.desc;
-  const int64_t keep_cap = ws.cap_desc;
-  ws.desc = nullptr;
   free_ws(ws);
-  ws.desc = keep_desc;
-  ws.cap_desc = keep_cap;
-  const int64_t mf = maxflag_for((int)kk, h->ix.ntiles);
-  HIP_TRY(hipMalloc(&ws.cand, sizeof(uint64_t) * q * h->ix.ntiles * kTileM), "hipMalloc(cand)");
+  const int64_t nt = h->ix.ntiles;
+  const int64_t mf = maxflag_for((int)kk, nt);
+  const int32_t C = list_cap_for(kk);
+  HIP_TRY(hipMalloc(&ws.cand, sizeof(uint64_t) * q * nt * kTileM), "hipMalloc(cand)");
   HIP_TRY(hipMalloc(&ws.theta, sizeof(uint64_t) * q), "hipMalloc(theta)");
+  HIP_TRY(hipMalloc(&ws.list, sizeof(uint64_t) * q * C), "hipMalloc(list)");
+  HIP_TRY(hipMalloc(&ws.list_cnt, sizeof(int32_t) * q), "hipMalloc(list_cnt)");
+  HIP_TRY(hipMalloc(&ws.fb, sizeof(int32_t) * q), "hipMalloc(fb)");
   HIP_TRY(hipMalloc(&ws.cand2, sizeof(uint64_t) * q * mf * kk), "hipMalloc(cand2)");
   HIP_TRY(hipMalloc(&ws.flag_tiles, sizeof(int32_t) * q * mf), "hipMalloc(flag_tiles)");
   HIP_TRY(hipMalloc(&ws.nflag, sizeof(int32_t) * q), "hipMalloc(nflag)");
-  HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
   HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
-  HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * 16), "hipMalloc(wctr)");
-  HIP_TRY(hipMalloc(&ws.ovq, sizeof(int32_t) * q * h->ix.ntiles), "hipMalloc(ovq)");
+  HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
+  HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * 4), "hipMemset(counters)");
+  ws.list_cap = C;
   ws.cap_q = q;
   ws.cap_k = kk;
   return BM25_OK;
@@ -181,7 +183,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   if (rc) return rc;
   EventPair* ev = next_events(h);
   if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
-  HIP_TRY(launch_score_tiles(h->ix, d_queries, Q, T, k, h->ws, st), "score_tiles launch");
+  HIP_TRY(launch_score(h->ix, d_queries, Q, T, k, h->ws, st), "score launch");
   if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
   HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, h->ws, d_docs, d_scores, st), "select launch");
   if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
@@ -190,6 +192,14 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
     h->searches += 1;
   }
   return BM25_OK;
+}
+
+// Counters of the last search (caller holds h->mu); the search may run on a
+// caller's stream, so synchronise the device.
+void read_counters(bm25_index* h, int32_t (&cnt)[4]) {
+  if (!h->ws.counters) return;
+  hipDeviceSynchronize();
+  hipMemcpy(cnt, h->ws.counters, sizeof cnt, hipMemcpyDeviceToHost);
 }
 
 int check_k(const bm25_index* h, int64_t k) {
@@ -240,8 +250,8 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     if (ip[t + 1] - ip[t] > n_docs)
       return fail(BM25_EINVAL, "column %lld has more entries than n_docs", (long long)t);
   }
-  int shift = env_int("BM25_TILE_SHIFT", 13);
-  if (!tile_shift_supported(shift)) return fail(BM25_EINVAL, "BM25_TILE_SHIFT=%d not compiled (12..15)", shift);
+  int shift = env_int("BM25_TILE_SHIFT", kDefaultTileShift);
+  if (!tile_shift_supported(shift)) return fail(BM25_EINVAL, "BM25_TILE_SHIFT=%d not compiled (10..11)", shift);
   const int64_t ntiles = (n_docs + (1LL << shift) - 1) >> shift;
   if (ntiles > 65536) return fail(BM25_EINVAL, "n_docs=%lld needs %lld tiles (> 65536)", (long long)n_docs, (long long)ntiles);
 
@@ -440,15 +450,23 @@ int bm25_profile_read(bm25_index* h, double* score_ms_total, int64_t* score_laun
   hipSetDevice(h->ix.device);
   harvest_events(h);
   int32_t cnt[4] = {0, 0, 0, 0};
-  if (h->ws.counters) {
-    hipMemcpyAsync(cnt, h->ws.counters, sizeof cnt, hipMemcpyDeviceToHost, h->stream);
-    hipStreamSynchronize(h->stream);
-  }
+  read_counters(h, cnt);
   if (score_ms_total) *score_ms_total = h->score_ms;
   if (score_launches) *score_launches = h->score_launches;
   if (total_ms) *total_ms = h->total_ms;
   if (searches) *searches = h->searches;
-  if (rescored_tiles) *rescored_tiles = cnt[0];  // items queued by the last search
+  if (rescored_tiles) *rescored_tiles = cnt[3];  // tiles re-scored by the last search
+  return BM25_OK;
+}
+
+int bm25_search_stats(bm25_index* h, int64_t* rescored_tiles, int64_t* fallback_queries) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  int32_t cnt[4] = {0, 0, 0, 0};
+  read_counters(h, cnt);
+  if (rescored_tiles) *rescored_tiles = cnt[3];
+  if (fallback_queries) *fallback_queries = cnt[2];
   return BM25_OK;
 }
 
