@@ -322,6 +322,113 @@ __device__ __forceinline__ int64_t tile_of(int64_t ti, int P) {
 }
 
 // ---------------------------------------------------------------------------
+// Software-pipelined pieces of the scatter phase (score_pipe_kernel).  An
+// item's dependent loads — query terms -> (indptr, rel) -> postings — are
+// issued three, two and one items ahead of its adds, so the latency of each
+// level hides behind the work of the items in between.  Every stage issues a
+// fixed number of loads, none under a branch (lanes with nothing to load read
+// a valid dummy address), so the compiler's vmcnt waits stay counted instead
+// of draining the queue.
+// ---------------------------------------------------------------------------
+struct Desc {  // lane s < T: raw segment bounds of query term s
+  int64_t ip;
+  uint32_t r0, r1;
+  bool ok;
+};
+
+__device__ __forceinline__ Desc load_desc(const IndexArgs& a, int32_t term, int64_t tile) {
+  Desc d;
+  d.ok = term >= 0 && term < a.V;  // negative ids are padding (bm25_native.py:151)
+  const int64_t t = d.ok ? term : 0;
+  const uint32_t* r = a.rel + t * (a.ntiles + 1) + tile;
+  d.ip = a.indptr[t];
+  d.r0 = r[0];
+  d.r1 = r[1];
+  return d;
+}
+
+struct Seg {  // an item's segments as one stream (lane s: term s)
+  int64_t delta;   // posting index - stream position
+  uint32_t start;  // stream position of term s
+  uint32_t total;  // postings of the item (uniform)
+};
+
+__device__ __forceinline__ Seg make_seg(const Desc& d, int T) {
+  const uint32_t len = (lane_id() < T && d.ok) ? d.r1 - d.r0 : 0u;
+  const uint32_t incl = wave_incl_scan(len);
+  Seg s;
+  s.start = incl - len;
+  s.delta = d.ip + (int64_t)d.r0 - (int64_t)s.start;
+  s.total = lane_u32(incl, T - 1);
+  return s;
+}
+
+// Term range [first, last] of stream row [rs, rs + 64) (rs < total), and
+// this lane's term / posting offset.
+__device__ __forceinline__ void row_terms(const Seg& sg, int T, uint32_t rs, int& s_cur, int& last,
+                                          int& s, int64_t& d) {
+  while (s_cur + 1 < T && lane_u32(sg.start, s_cur + 1) <= rs) ++s_cur;
+  const uint32_t p = rs + lane_id();
+  const uint32_t re = min(rs + 64u, sg.total);
+  s = s_cur;
+  last = s_cur;
+  d = lane_i64(sg.delta, s_cur);
+  for (int sc = s_cur + 1; sc < T && lane_u32(sg.start, sc) < re; ++sc) {
+    if (p >= lane_u32(sg.start, sc)) {
+      s = sc;
+      d = lane_i64(sg.delta, sc);
+    }
+    last = sc;
+  }
+}
+
+// Loads of stream rows [r0, r0 + 64*kJ): lt = LDS slot | term << 16, v = score.
+__device__ __forceinline__ void issue_rows(const IndexArgs& a, const Seg& sg, int T, uint32_t r0,
+                                           uint32_t (&lt)[kJ], float (&v)[kJ]) {
+  const uint32_t lane = lane_id();
+  int s_cur = 0;
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t rs = r0 + 64u * j;
+    int s = 0, last = 0;
+    int64_t d = 0;
+    if (rs < sg.total) row_terms(sg, T, rs, s_cur, last, s, d);
+    const uint32_t p = rs + lane;
+    const int64_t g = p < sg.total ? (int64_t)p + d : 0;
+    lt[j] = (uint32_t)a.ldoc[g] | ((uint32_t)s << 16);
+    v[j] = a.val[g];
+  }
+}
+
+// Adds of the rows loaded by issue_rows, in stream order.
+__device__ __forceinline__ void add_rows(float* acc, const Seg& sg, int T, uint32_t r0,
+                                         const uint32_t (&lt)[kJ], const float (&v)[kJ]) {
+  const uint32_t lane = lane_id();
+  int s_cur = 0;
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t rs = r0 + 64u * j;
+    if (rs >= sg.total) break;
+    int s, last;
+    int64_t d;
+    row_terms(sg, T, rs, s_cur, last, s, d);
+    const bool live = rs + lane < sg.total;
+    const uint32_t dl = lt[j] & 0xFFFFu;
+    if (s_cur == last) {
+      if (live) lds_add(acc + dl, v[j]);
+    } else {
+      const int ts = (int)(lt[j] >> 16);
+      for (int sc = s_cur; sc <= last; ++sc)
+        if (live && ts == sc) lds_add(acc + dl, v[j]);
+    }
+  }
+}
+
+struct Cursor {  // item it0 + n*stride as (ti, qi)
+  int64_t ti, qi;
+};
+
+// ---------------------------------------------------------------------------
 // Persistent score kernel: kWaves independent waves per workgroup, each with a
 // private 2^S-float LDS accumulator.  The phase's items are tile-major
 // (item = ti * nq + qi) and split into 8 contiguous ranges, one per XCD
@@ -363,6 +470,114 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
       emit_above<S>(fv, tile, a.n_docs, theta[qi], list + qi * C, list_cnt + qi, C);
     else
       select_top<S>(fv, tile, a.n_docs, kTileM, cand + (qi * nt + ti) * kTileM);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined persistent score kernel (1 <= T <= 64): same items, same order
+// and same arithmetic as score_wave_kernel, with iteration n issuing
+//   (1) the query terms of item n+3,
+//   (2) the (indptr, rel) segment bounds of item n+2,
+//   (3) the first kJ posting rows of item n+1,
+// and then (4) adding item n's rows (further rows of a heavy item are loaded
+// in place) and selecting / emitting its candidates.
+// ---------------------------------------------------------------------------
+template <int S, int PH>
+__global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
+    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, Stage sg,
+    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
+    int32_t* __restrict__ list_cnt, int32_t C) {
+  constexpr int D = 1 << S;
+  __shared__ __attribute__((aligned(16))) float acc_all[kWaves * D];
+  const int wave = uniform((int)(threadIdx.x >> 6));
+  float* acc = acc_all + wave * D;
+  const int64_t nq = sg.nq_dev ? (int64_t)*sg.nq_dev : (int64_t)sg.nq_host;
+  const int P = sg.P;
+  const int64_t nS = (a.ntiles + P - 1) / P;
+  const int64_t nt = PH == kAll ? a.ntiles : (PH == kSample ? nS : a.ntiles - nS);
+  const int64_t nitems = nt * nq;
+  const int64_t per = (nitems + 7) >> 3;
+  const int64_t grp = blockIdx.x & 7;
+  const int64_t lo = grp * per;
+  const int64_t hi = min(nitems, lo + per);
+  const int64_t stride = (int64_t)(gridDim.x >> 3) * kWaves;
+  const int64_t it0 = lo + (int64_t)(blockIdx.x >> 3) * kWaves + wave;
+  if (it0 >= hi) return;  // wave-uniform; no barriers in this kernel
+  const int64_t count = (hi - it0 + stride - 1) / stride;
+  const int64_t sdiv = stride / nq, smod = stride - sdiv * nq;
+  const int tl = min(lane_id(), T - 1);
+
+  // cursor of item n+1 from item n's (stays on the last item past the end,
+  // so every stage keeps loading valid addresses)
+  auto next = [&](Cursor c, int64_t n) -> Cursor {
+    if (n + 1 < count) {
+      c.ti += sdiv;
+      c.qi += smod;
+      if (c.qi >= nq) {
+        c.qi -= nq;
+        ++c.ti;
+      }
+    }
+    return c;
+  };
+  auto terms_of = [&](const Cursor& c) -> int32_t {
+    const int64_t q = sg.qmap ? (int64_t)sg.qmap[c.qi] : c.qi;
+    return queries[q * T + tl];
+  };
+
+  zero_acc<S>(acc);
+  Cursor cD;
+  cD.ti = it0 / nq;
+  cD.qi = it0 - cD.ti * nq;
+  Cursor cC = next(cD, 0), cB = next(cC, 1), cA = next(cB, 2);
+  // prologue: item 0's rows, item 1's bounds, item 2's terms
+  const int32_t tm0 = terms_of(cD), tm1 = terms_of(cC);
+  int32_t tmB = terms_of(cB);
+  Seg sD = make_seg(load_desc(a, tm0, tile_of<PH>(cD.ti, P)), T);
+  Desc dC = load_desc(a, tm1, tile_of<PH>(cC.ti, P));
+  uint32_t ltD[kJ];
+  float vD[kJ];
+  issue_rows(a, sD, T, 0, ltD, vD);
+  uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
+
+  for (int64_t n = 0; n < count; ++n) {
+    // (1) terms of item n+3, (2) bounds of item n+2, (3) rows of item n+1
+    const int32_t tmA = terms_of(cA);
+    const Desc dB = load_desc(a, tmB, tile_of<PH>(cB.ti, P));
+    const Seg sC = make_seg(dC, T);
+    uint32_t ltC[kJ];
+    float vC[kJ];
+    issue_rows(a, sC, T, 0, ltC, vC);
+    const uint64_t thC = PH == kRest ? theta[cC.qi] : 0ull;
+    // (4) item n
+    const int64_t tile = tile_of<PH>(cD.ti, P);
+    add_rows(acc, sD, T, 0, ltD, vD);
+    for (uint32_t r0 = 64u * kJ; r0 < sD.total; r0 += 64u * kJ) {  // heavy item
+      uint32_t ltX[kJ];
+      float vX[kJ];
+      issue_rows(a, sD, T, r0, ltX, vX);
+      add_rows(acc, sD, T, r0, ltX, vX);
+    }
+    float fv[D / 64];
+    take_entries<S>(acc, fv);
+    if (PH == kRest)
+      emit_above<S>(fv, tile, a.n_docs, thD, list + cD.qi * C, list_cnt + cD.qi, C);
+    else
+      select_top<S>(fv, tile, a.n_docs, kTileM, cand + (cD.qi * nt + cD.ti) * kTileM);
+    // rotate the pipeline
+    cD = cC;
+    cC = cB;
+    cB = cA;
+    cA = next(cA, n + 3);
+    tmB = tmA;
+    dC = dB;
+    sD = sC;
+    thD = thC;
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+      ltD[j] = ltC[j];
+      vD[j] = vC[j];
+    }
   }
 }
 
@@ -751,19 +966,35 @@ int sample_stride(int64_t ntiles, int k) {
   return 1;
 }
 
+template <int S, int PH, class K>
+static int persistent_grid(K kernel) {
+  int dev = 0, cus = 0, occ = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 64 * kWaves, 0);
+  const char* e = getenv("BM25_WG_PER_CU");
+  if (e) occ = atoi(e);
+  return ((cus * (occ > 0 ? occ : 1) + 7) / 8) * 8;  // every resident slot, a multiple of 8
+}
+
+// The pipelined kernel serves queries of 1..64 terms (BM25_NO_PIPE=1 forces
+// the plain one, which also serves longer queries).
+static bool use_pipe(int64_t T) {
+  static const bool off = getenv("BM25_NO_PIPE") != nullptr;
+  return !off && T >= 1 && T <= kGroup;
+}
+
 template <int S, int PH>
 static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
                         const Workspace& ws, hipStream_t st) {
-  static int grid = 0;  // persistent grid: every resident wave slot, a multiple of 8
-  if (grid == 0) {
-    int dev = 0, cus = 0, occ = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, score_wave_kernel<S, PH>, 64 * kWaves, 0);
-    const char* e = getenv("BM25_WG_PER_CU");
-    if (e) occ = atoi(e);
-    grid = ((cus * (occ > 0 ? occ : 1) + 7) / 8) * 8;
+  if (use_pipe(T)) {
+    static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH>);
+    hipLaunchKernelGGL((score_pipe_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0,
+                       st, args_of(ix), q, (int32_t)T, sg, ws.theta, ws.cand, ws.list,
+                       ws.list_cnt, ws.list_cap);
+    return;
   }
+  static const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
   hipLaunchKernelGGL((score_wave_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0, st,
                      args_of(ix), q, (int32_t)T, sg, ws.theta, ws.cand, ws.list, ws.list_cnt,
                      ws.list_cap);

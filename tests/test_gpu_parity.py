@@ -282,6 +282,7 @@ def test_config3_full_index_subset_parity(gpu):
 @pytest.mark.parametrize("variant", [
     {}, {"BM25_SAMPLE_P": "1"}, {"BM25_SAMPLE_P": "2"}, {"BM25_SAMPLE_P": "16"},
     {"BM25_LIST_CAP": "8"}, {"BM25_TILE_SHIFT": "10", "BM25_LIST_CAP": "40"},
+    {"BM25_NO_PIPE": "1"}, {"BM25_NO_PIPE": "1", "BM25_LIST_CAP": "8"},
 ])
 def test_kernel_variants_bit_exact(gpu, variant, monkeypatch):
     """Every search configuration gives the oracle's bits: sampling strides
