@@ -402,8 +402,14 @@ __device__ __forceinline__ void issue_rows(const IndexArgs& a, const Seg& sg, in
 
 // Adds of the rows loaded by issue_rows, in stream order.
 __device__ __forceinline__ void add_rows(float* acc, const Seg& sg, int T, uint32_t r0,
-                                         const uint32_t (&lt)[kJ], const float (&v)[kJ]) {
+                                         const uint32_t (&lt)[kJ], const float (&v)[kJ],
+                                         int mode = 0) {
   const uint32_t lane = lane_id();
+  if (mode & 1) {  // ablation: consume the loads, no adds
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(lt[j]), "v"(v[j]));
+    return;
+  }
   int s_cur = 0;
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
@@ -414,7 +420,11 @@ __device__ __forceinline__ void add_rows(float* acc, const Seg& sg, int T, uint3
     row_terms(sg, T, rs, s_cur, last, s, d);
     const bool live = rs + lane < sg.total;
     const uint32_t dl = lt[j] & 0xFFFFu;
-    if (s_cur == last) {
+    if (mode & 2) {  // read-add-write instead of the LDS atomic (same order, same bits)
+      const int ts = (int)(lt[j] >> 16);
+      for (int sc = s_cur; sc <= last; ++sc)
+        if (live && ts == sc) acc[dl] = acc[dl] + v[j];
+    } else if (s_cur == last) {
       if (live) lds_add(acc + dl, v[j]);
     } else {
       const int ts = (int)(lt[j] >> 16);
@@ -486,7 +496,7 @@ template <int S, int PH>
 __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t T, Stage sg,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
-    int32_t* __restrict__ list_cnt, int32_t C) {
+    int32_t* __restrict__ list_cnt, int32_t C, int mode) {
   constexpr int D = 1 << S;
   __shared__ __attribute__((aligned(16))) float acc_all[kWaves * D];
   const int wave = uniform((int)(threadIdx.x >> 6));
@@ -551,16 +561,18 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     const uint64_t thC = PH == kRest ? theta[cC.qi] : 0ull;
     // (4) item n
     const int64_t tile = tile_of<PH>(cD.ti, P);
-    add_rows(acc, sD, T, 0, ltD, vD);
+    add_rows(acc, sD, T, 0, ltD, vD, mode);
     for (uint32_t r0 = 64u * kJ; r0 < sD.total; r0 += 64u * kJ) {  // heavy item
       uint32_t ltX[kJ];
       float vX[kJ];
       issue_rows(a, sD, T, r0, ltX, vX);
-      add_rows(acc, sD, T, r0, ltX, vX);
+      add_rows(acc, sD, T, r0, ltX, vX, mode);
     }
     float fv[D / 64];
     take_entries<S>(acc, fv);
-    if (PH == kRest)
+    if (mode & 4) {  // ablation: no selection
+      if (fv[0] == 12345.f) cand[0] = 0;
+    } else if (PH == kRest)
       emit_above<S>(fv, tile, a.n_docs, thD, list + cD.qi * C, list_cnt + cD.qi, C);
     else
       select_top<S>(fv, tile, a.n_docs, kTileM, cand + (cD.qi * nt + cD.ti) * kTileM);
@@ -989,9 +1001,10 @@ static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const S
                         const Workspace& ws, hipStream_t st) {
   if (use_pipe(T)) {
     static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH>);
+    static const int mode = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
     hipLaunchKernelGGL((score_pipe_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0,
                        st, args_of(ix), q, (int32_t)T, sg, ws.theta, ws.cand, ws.list,
-                       ws.list_cnt, ws.list_cap);
+                       ws.list_cnt, ws.list_cap, mode);
     return;
   }
   static const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
