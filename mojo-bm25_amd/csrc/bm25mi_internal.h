@@ -2,9 +2,9 @@
 // (bm25mi_capi.cpp) and the gfx950 kernels (bm25mi_kernels.hip).
 //
 // Device layout of one index, tiles of D = 2^S docs (S = 11):
-//   val   f32 [nnz+pad]      the CSC `data` array, unchanged order (term-major,
+//   val   f32 [nnz+64]       the CSC `data` array, unchanged order (term-major,
 //                            doc-ascending inside a term)
-//   ldoc  u16 [nnz+pad]      LDS slot of the doc inside its tile: acc_slot()
+//   ldoc  u16 [nnz+64]       LDS slot of the doc inside its tile: acc_slot()
 //                            of the doc's tile-local id; the tile of a posting
 //                            is implied by its position
 //   indptr i64 [V+1]         CSC column pointers
@@ -42,7 +42,8 @@ constexpr int kTileM = 4;
 constexpr int kMaxK = 4096;
 // Merge kernel LDS: number of u64 keys sorted at once.
 constexpr int kMergeP = 8192;
-// Posting arrays carry a small zeroed tail (loads are masked, not clamped).
+// Posting arrays carry 64 pad postings (slot = lane, score +0.0): a lane past
+// its row's segment reads pad posting `lane` and adds +0.0 (a no-op).
 constexpr int64_t kPostingPad = 64;
 // Default tile: 2^11 = 2048 docs, one wavefront's LDS accumulator (8 KB).
 constexpr int kDefaultTileShift = 11;

@@ -43,10 +43,11 @@ struct IndexArgs {
   const uint16_t* ldoc;
   const float* val;
   int64_t V, ntiles, n_docs;
+  int64_t pad;  // index of the 64 pad postings (slot = lane, score +0.0)
 };
 
 static IndexArgs args_of(const DevIndex& ix) {
-  return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs};
+  return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs, ix.nnz};
 }
 
 // One search stage of candidate selection (see the merge kernels).
@@ -347,91 +348,68 @@ __device__ __forceinline__ Desc load_desc(const IndexArgs& a, int32_t term, int6
   return d;
 }
 
-struct Seg {  // an item's segments as one stream (lane s: term s)
-  int64_t delta;   // posting index - stream position
-  uint32_t start;  // stream position of term s
-  uint32_t total;  // postings of the item (uniform)
+// An item's posting rows: each query term's segment is cut into rows of 64
+// postings (one per lane), so a row belongs to one term and its adds need no
+// term mask.  Lane j of the table describes row j0 + j of the item.
+struct Rows {
+  int64_t base;    // posting index of the row's first posting
+  uint32_t cnt;    // postings in the row (0: past the item's rows)
+  uint32_t nrows;  // rows of the item (uniform)
 };
 
-__device__ __forceinline__ Seg make_seg(const Desc& d, int T) {
-  const uint32_t len = (lane_id() < T && d.ok) ? d.r1 - d.r0 : 0u;
-  const uint32_t incl = wave_incl_scan(len);
-  Seg s;
-  s.start = incl - len;
-  s.delta = d.ip + (int64_t)d.r0 - (int64_t)s.start;
-  s.total = lane_u32(incl, T - 1);
-  return s;
-}
-
-// Term range [first, last] of stream row [rs, rs + 64) (rs < total), and
-// this lane's term / posting offset.
-__device__ __forceinline__ void row_terms(const Seg& sg, int T, uint32_t rs, int& s_cur, int& last,
-                                          int& s, int64_t& d) {
-  while (s_cur + 1 < T && lane_u32(sg.start, s_cur + 1) <= rs) ++s_cur;
-  const uint32_t p = rs + lane_id();
-  const uint32_t re = min(rs + 64u, sg.total);
-  s = s_cur;
-  last = s_cur;
-  d = lane_i64(sg.delta, s_cur);
-  for (int sc = s_cur + 1; sc < T && lane_u32(sg.start, sc) < re; ++sc) {
-    if (p >= lane_u32(sg.start, sc)) {
-      s = sc;
-      d = lane_i64(sg.delta, sc);
-    }
-    last = sc;
-  }
-}
-
-// Loads of stream rows [r0, r0 + 64*kJ): lt = LDS slot | term << 16, v = score.
-__device__ __forceinline__ void issue_rows(const IndexArgs& a, const Seg& sg, int T, uint32_t r0,
-                                           uint32_t (&lt)[kJ], float (&v)[kJ]) {
+__device__ __forceinline__ Rows make_rows(const Desc& d, int T, uint32_t j0) {
   const uint32_t lane = lane_id();
-  int s_cur = 0;
+  const uint32_t len = ((int)lane < T && d.ok) ? d.r1 - d.r0 : 0u;
+  const int64_t beg = d.ip + (int64_t)d.r0;
+  const uint32_t nr = (len + 63u) >> 6;
+  const uint32_t rincl = wave_incl_scan(nr);
+  Rows r;
+  r.nrows = lane_u32(rincl, T - 1);
+  const uint32_t j = j0 + lane;  // the row this lane describes
+  int64_t b = 0;
+  uint32_t rs = 0, l = 0;
+  for (int s = 0; s < T; ++s) {  // term of row j: rincl[s] - nr[s] <= j < rincl[s]
+    const uint32_t e = lane_u32(rincl, s), st = e - lane_u32(nr, s);
+    if (j >= st && j < e) {
+      b = lane_i64(beg, s);
+      rs = st;
+      l = lane_u32(len, s);
+    }
+  }
+  const uint32_t k = j - rs;  // row index inside its term
+  r.base = b + 64 * (int64_t)k;
+  r.cnt = j < r.nrows ? min(64u, l - 64u * k) : 0u;
+  return r;
+}
+
+// Loads of table rows [j0, j0 + kJ): slot + score per lane.  Lanes past a
+// row's postings read the pad posting of their lane (slot = lane, score
+// +0.0): adding +0.0 leaves any accumulator's bits unchanged (an accumulator
+// is never -0.0), so the adds need no mask either.
+__device__ __forceinline__ void issue_rows(const IndexArgs& a, const Rows& R, int j0,
+                                           uint32_t (&ld)[kJ], float (&v)[kJ]) {
+  const uint32_t lane = lane_id();
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
-    const uint32_t rs = r0 + 64u * j;
-    int s = 0, last = 0;
-    int64_t d = 0;
-    if (rs < sg.total) row_terms(sg, T, rs, s_cur, last, s, d);
-    const uint32_t p = rs + lane;
-    const int64_t g = p < sg.total ? (int64_t)p + d : 0;
-    lt[j] = (uint32_t)a.ldoc[g] | ((uint32_t)s << 16);
+    const int64_t base = lane_i64(R.base, j0 + j);
+    const uint32_t cnt = lane_u32(R.cnt, j0 + j);
+    const int64_t g = lane < cnt ? base + lane : a.pad + lane;
+    ld[j] = a.ldoc[g];
     v[j] = a.val[g];
   }
 }
 
-// Adds of the rows loaded by issue_rows, in stream order.
-__device__ __forceinline__ void add_rows(float* acc, const Seg& sg, int T, uint32_t r0,
-                                         const uint32_t (&lt)[kJ], const float (&v)[kJ],
-                                         int mode = 0) {
-  const uint32_t lane = lane_id();
+// The first n (uniform) of the loaded rows, in order.
+__device__ __forceinline__ void add_rows(float* acc, const uint32_t (&ld)[kJ], const float (&v)[kJ],
+                                         uint32_t n, int mode) {
   if (mode & 1) {  // ablation: consume the loads, no adds
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(lt[j]), "v"(v[j]));
+    for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
     return;
   }
-  int s_cur = 0;
 #pragma unroll
-  for (int j = 0; j < kJ; ++j) {
-    const uint32_t rs = r0 + 64u * j;
-    if (rs >= sg.total) break;
-    int s, last;
-    int64_t d;
-    row_terms(sg, T, rs, s_cur, last, s, d);
-    const bool live = rs + lane < sg.total;
-    const uint32_t dl = lt[j] & 0xFFFFu;
-    if (mode & 2) {  // read-add-write instead of the LDS atomic (same order, same bits)
-      const int ts = (int)(lt[j] >> 16);
-      for (int sc = s_cur; sc <= last; ++sc)
-        if (live && ts == sc) acc[dl] = acc[dl] + v[j];
-    } else if (s_cur == last) {
-      if (live) lds_add(acc + dl, v[j]);
-    } else {
-      const int ts = (int)(lt[j] >> 16);
-      for (int sc = s_cur; sc <= last; ++sc)
-        if (live && ts == sc) lds_add(acc + dl, v[j]);
-    }
-  }
+  for (int j = 0; j < kJ; ++j)
+    if ((uint32_t)j < n) lds_add(acc + ld[j], v[j]);
 }
 
 struct Cursor {  // item it0 + n*stride as (ti, qi)
@@ -484,13 +462,13 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined persistent score kernel (1 <= T <= 64): same items, same order
-// and same arithmetic as score_wave_kernel, with iteration n issuing
+// Pipelined persistent score kernel (1 <= T <= 64): same items, same order,
+// same per-document add order as score_wave_kernel, with iteration n issuing
 //   (1) the query terms of item n+3,
 //   (2) the (indptr, rel) segment bounds of item n+2,
-//   (3) the first kJ posting rows of item n+1,
-// and then (4) adding item n's rows (further rows of a heavy item are loaded
-// in place) and selecting / emitting its candidates.
+//   (3) item n's second block of kJ posting rows and item n+1's first block,
+// and then (4) adding item n's rows (a heavy item's further rows are loaded in
+// place) and selecting / emitting its candidates.
 // ---------------------------------------------------------------------------
 template <int S, int PH>
 __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
@@ -540,50 +518,64 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   cD.ti = it0 / nq;
   cD.qi = it0 - cD.ti * nq;
   Cursor cC = next(cD, 0), cB = next(cC, 1), cA = next(cB, 2);
-  // prologue: item 0's rows, item 1's bounds, item 2's terms
+  // prologue: item 0's first rows, item 1's bounds, item 2's terms
   const int32_t tm0 = terms_of(cD), tm1 = terms_of(cC);
   int32_t tmB = terms_of(cB);
-  Seg sD = make_seg(load_desc(a, tm0, tile_of<PH>(cD.ti, P)), T);
+  Desc dD = load_desc(a, tm0, tile_of<PH>(cD.ti, P));
   Desc dC = load_desc(a, tm1, tile_of<PH>(cC.ti, P));
+  Rows rD = make_rows(dD, T, 0);
   uint32_t ltD[kJ];
   float vD[kJ];
-  issue_rows(a, sD, T, 0, ltD, vD);
+  issue_rows(a, rD, 0, ltD, vD);
   uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
 
   for (int64_t n = 0; n < count; ++n) {
-    // (1) terms of item n+3, (2) bounds of item n+2, (3) rows of item n+1
+    // (1) terms of item n+3, (2) bounds of item n+2
     const int32_t tmA = terms_of(cA);
     const Desc dB = load_desc(a, tmB, tile_of<PH>(cB.ti, P));
-    const Seg sC = make_seg(dC, T);
+    // (3) item n's second row block (issued before item n+1's rows so that
+    //     its wait does not cover them), then item n+1's first rows
+    const uint32_t nrD = rD.nrows;
+    uint32_t ltX[kJ];
+    float vX[kJ];
+    if (nrD > kJ) issue_rows(a, rD, kJ, ltX, vX);
+    const Rows rC = make_rows(dC, T, 0);
     uint32_t ltC[kJ];
     float vC[kJ];
-    issue_rows(a, sC, T, 0, ltC, vC);
+    issue_rows(a, rC, 0, ltC, vC);
     const uint64_t thC = PH == kRest ? theta[cC.qi] : 0ull;
-    // (4) item n
+    // (4) item n: adds in row order, then selection
     const int64_t tile = tile_of<PH>(cD.ti, P);
-    add_rows(acc, sD, T, 0, ltD, vD, mode);
-    for (uint32_t r0 = 64u * kJ; r0 < sD.total; r0 += 64u * kJ) {  // heavy item
-      uint32_t ltX[kJ];
-      float vX[kJ];
-      issue_rows(a, sD, T, r0, ltX, vX);
-      add_rows(acc, sD, T, r0, ltX, vX, mode);
+    add_rows(acc, ltD, vD, min(nrD, (uint32_t)kJ), mode);
+    if (nrD > kJ) add_rows(acc, ltX, vX, min(nrD - kJ, (uint32_t)kJ), mode);
+    if (nrD > 2 * kJ) {  // heavy item: the remaining rows, block by block
+      Rows t = rD;
+      for (uint32_t j = 2 * kJ; j < nrD; j += kJ) {
+        if ((j & 63) == 0) t = make_rows(dD, T, j);
+        uint32_t ltY[kJ];
+        float vY[kJ];
+        issue_rows(a, t, (int)(j & 63), ltY, vY);
+        add_rows(acc, ltY, vY, min(nrD - j, (uint32_t)kJ), mode);
+      }
     }
     float fv[D / 64];
     take_entries<S>(acc, fv);
     if (mode & 4) {  // ablation: no selection
       if (fv[0] == 12345.f) cand[0] = 0;
-    } else if (PH == kRest)
+    } else if (PH == kRest) {
       emit_above<S>(fv, tile, a.n_docs, thD, list + cD.qi * C, list_cnt + cD.qi, C);
-    else
+    } else {
       select_top<S>(fv, tile, a.n_docs, kTileM, cand + (cD.qi * nt + cD.ti) * kTileM);
+    }
     // rotate the pipeline
     cD = cC;
     cC = cB;
     cB = cA;
     cA = next(cA, n + 3);
     tmB = tmA;
+    dD = dC;
     dC = dB;
-    sD = sC;
+    rD = rC;
     thD = thC;
 #pragma unroll
     for (int j = 0; j < kJ; ++j) {
