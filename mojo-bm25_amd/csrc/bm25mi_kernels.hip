@@ -407,6 +407,21 @@ __device__ __forceinline__ void add_rows(float* acc, const uint32_t (&ld)[kJ], c
     for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
     return;
   }
+  if (mode & 8) {  // row-at-a-time read-add-write (same order, same bits)
+#pragma unroll
+    for (int j = 0; j < kJ; ++j)
+      if ((uint32_t)j < n) acc[ld[j]] = acc[ld[j]] + v[j];
+    return;
+  }
+  if (mode & 16) {  // timing only (wrong across term boundaries): all reads, then all writes
+    float x[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) x[j] = (uint32_t)j < n ? acc[ld[j]] : 0.f;
+#pragma unroll
+    for (int j = 0; j < kJ; ++j)
+      if ((uint32_t)j < n) acc[ld[j]] = x[j] + v[j];
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < kJ; ++j)
     if ((uint32_t)j < n) lds_add(acc + ld[j], v[j]);
