@@ -399,7 +399,11 @@ __device__ __forceinline__ void issue_rows(const IndexArgs& a, const Rows& R, in
   }
 }
 
-// The first n (uniform) of the loaded rows, in order.
+// The first n (uniform) of the loaded rows, in order: ds_read, add,
+// ds_write per row.  A row's docs are distinct (one term), and the LDS
+// executes a wave's instructions in order, so row j+1's read sees row j's
+// write.  (An LDS float atomic does the same add at ~2.5x the cost on
+// gfx950: 23.8 vs 10.9 ms for the config-3 score pass, BM25_ABLATE=8.)
 __device__ __forceinline__ void add_rows(float* acc, const uint32_t (&ld)[kJ], const float (&v)[kJ],
                                          uint32_t n, int mode) {
   if (mode & 1) {  // ablation: consume the loads, no adds
@@ -407,24 +411,15 @@ __device__ __forceinline__ void add_rows(float* acc, const uint32_t (&ld)[kJ], c
     for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
     return;
   }
-  if (mode & 8) {  // row-at-a-time read-add-write (same order, same bits)
+  if (mode & 8) {  // ablation: LDS float atomics
 #pragma unroll
     for (int j = 0; j < kJ; ++j)
-      if ((uint32_t)j < n) acc[ld[j]] = acc[ld[j]] + v[j];
-    return;
-  }
-  if (mode & 16) {  // timing only (wrong across term boundaries): all reads, then all writes
-    float x[kJ];
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) x[j] = (uint32_t)j < n ? acc[ld[j]] : 0.f;
-#pragma unroll
-    for (int j = 0; j < kJ; ++j)
-      if ((uint32_t)j < n) acc[ld[j]] = x[j] + v[j];
+      if ((uint32_t)j < n) lds_add(acc + ld[j], v[j]);
     return;
   }
 #pragma unroll
   for (int j = 0; j < kJ; ++j)
-    if ((uint32_t)j < n) lds_add(acc + ld[j], v[j]);
+    if ((uint32_t)j < n) acc[ld[j]] = acc[ld[j]] + v[j];
 }
 
 struct Cursor {  // item it0 + n*stride as (ti, qi)
