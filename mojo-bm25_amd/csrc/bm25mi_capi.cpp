@@ -290,14 +290,7 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
   TRYC(hipMalloc(&ix.rel, sizeof(uint32_t) * std::max<int64_t>(rel_elems, 1)), "hipMalloc(rel)");
   TRYC(hipMalloc(&ix.ldoc, sizeof(uint16_t) * (nnz + kPostingPad)), "hipMalloc(ldoc)");
   TRYC(hipMalloc(&ix.val, sizeof(float) * (nnz + kPostingPad)), "hipMalloc(val)");
-  // pad postings: lane l of a row past its segment reads (slot l, +0.0)
-  static const std::vector<uint16_t> pad_slots = [] {
-    std::vector<uint16_t> v(kPostingPad);
-    for (int64_t i = 0; i < kPostingPad; ++i) v[i] = (uint16_t)i;
-    return v;
-  }();
-  TRYC(hipMemcpyAsync(ix.ldoc + nnz, pad_slots.data(), sizeof(uint16_t) * kPostingPad,
-                      hipMemcpyHostToDevice, h->stream), "H2D pad");
+  TRYC(hipMemsetAsync(ix.ldoc + nnz, 0, sizeof(uint16_t) * kPostingPad, h->stream), "hipMemset");
   TRYC(hipMemsetAsync(ix.val + nnz, 0, sizeof(float) * kPostingPad, h->stream), "hipMemset");
   TRYC(hipMalloc(&d_indices, sizeof(int32_t) * std::max<int64_t>(nnz, 1)), "hipMalloc(indices)");
   TRYC(hipMalloc(&d_err, sizeof(int32_t)), "hipMalloc(err)");

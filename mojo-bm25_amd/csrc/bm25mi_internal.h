@@ -4,9 +4,9 @@
 // Device layout of one index, tiles of D = 2^S docs (S = 11):
 //   val   f32 [nnz+64]       the CSC `data` array, unchanged order (term-major,
 //                            doc-ascending inside a term)
-//   ldoc  u16 [nnz+64]       LDS slot of the doc inside its tile: acc_slot()
-//                            of the doc's tile-local id; the tile of a posting
-//                            is implied by its position
+//   ldoc  u16 [nnz+64]       the doc's tile-local id (= its LDS accumulator
+//                            slot); the tile of a posting is implied by its
+//                            position
 //   indptr i64 [V+1]         CSC column pointers
 //   rel   u32 [V][ntiles+1]  rel[t][j] = first posting of term t whose doc is
 //                            in tile j or later, relative to indptr[t]
@@ -42,8 +42,7 @@ constexpr int kTileM = 4;
 constexpr int kMaxK = 4096;
 // Merge kernel LDS: number of u64 keys sorted at once.
 constexpr int kMergeP = 8192;
-// Posting arrays carry 64 pad postings (slot = lane, score +0.0): a lane past
-// its row's segment reads pad posting `lane` and adds +0.0 (a no-op).
+// Posting arrays carry a small tail (so posting 0 exists for an empty index).
 constexpr int64_t kPostingPad = 64;
 // Default tile: 2^11 = 2048 docs, one wavefront's LDS accumulator (8 KB).
 constexpr int kDefaultTileShift = 11;
@@ -74,15 +73,6 @@ struct Workspace {
   int32_t* counters = nullptr;   // [0]/[1] rescore queue length / pop cursor,
                                  // [2] fallback queries, [3] tiles re-scored this search
 };
-
-// Accumulator layout of a tile of D = 2^S docs: tile-local doc d belongs to
-// lane l = d / E of the wave (E = D / 64 entries per lane, so lane order ==
-// doc order) as entry e = d % E, stored at float index ((e/4)*64 + l)*4 + e%4:
-// the selection's float4 reads (j*64 + l) are conflict-free.
-__host__ __device__ inline uint32_t acc_slot(uint32_t d, int S) {
-  const uint32_t E = 1u << (S - 6);
-  return (((d & (E - 1u)) >> 2) << 8) | ((d >> (S - 6)) << 2) | (d & 3u);
-}
 
 // Flag slots per query: a flagged tile holds kTileM keys of the top-(k-1), so
 // at most (k-1)/kTileM tiles (and never more than the candidate tiles).

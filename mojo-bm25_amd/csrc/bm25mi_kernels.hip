@@ -43,11 +43,10 @@ struct IndexArgs {
   const uint16_t* ldoc;
   const float* val;
   int64_t V, ntiles, n_docs;
-  int64_t pad;  // index of the 64 pad postings (slot = lane, score +0.0)
 };
 
 static IndexArgs args_of(const DevIndex& ix) {
-  return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs, ix.nnz};
+  return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs};
 }
 
 // One search stage of candidate selection (see the merge kernels).
@@ -210,8 +209,15 @@ __device__ __forceinline__ void zero_acc(float* acc) {
   for (int j = 0; j < (1 << S) / 256; ++j) a4[j * 64 + lane_id()] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-// The lane's E = D/64 accumulators (tile-local docs lane*E .. lane*E+E-1, in
-// order), read with conflict-free float4 loads and cleared for the next item.
+// Accumulator layout: tile-local doc d lives at LDS float d (identity), so
+// the sorted doc ids of a posting row fall on consecutive banks.  A lane reads
+// float4 j*64 + lane: its entry e is tile-local doc entry_doc(e, lane) =
+// 256*(e/4) + 4*lane + e%4 (conflict-free ds_read_b128), cleared for the next
+// item as it is read.
+__device__ __forceinline__ uint32_t entry_doc(int e, uint32_t lane) {
+  return ((uint32_t)(e >> 2) << 8) | (lane << 2) | (uint32_t)(e & 3);
+}
+
 template <int S>
 __device__ __forceinline__ void take_entries(float* acc, float (&fv)[(1 << S) / 64]) {
   float4* a4 = reinterpret_cast<float4*>(acc);
@@ -229,40 +235,46 @@ __device__ __forceinline__ void take_entries(float* acc, float (&fv)[(1 << S) / 
 
 // ---------------------------------------------------------------------------
 // Exact selection: the m best keys of the tile, best first, into out[0..m).
-// Lane l owns docs [l*E, l*E + E), so "first lane, first entry" among equal
-// scores is the smallest doc id.  Docs past n_docs never qualify.
+// Each lane keeps its best entry (the first of equal keys: its entries are in
+// doc order); a round takes the wave's best key, then the smallest doc among
+// the lanes holding it, whose lane and entry follow from the doc id.  Docs
+// past n_docs never qualify.
 // ---------------------------------------------------------------------------
 template <int S>
 __device__ __forceinline__ void select_top(const float (&fv)[(1 << S) / 64], int64_t tile,
                                            int64_t n_docs, int m, uint64_t* __restrict__ out) {
   constexpr int E = (1 << S) / 64;
-  const int lane = lane_id();
-  const int64_t doc0 = (tile << S) + (int64_t)lane * E;
+  const uint32_t lane = lane_id();
+  const int64_t base = tile << S;
+  const int lim = (int)min<int64_t>(1 << S, n_docs - base);  // docs >= lim: past n_docs
   uint32_t key[E];
-  uint32_t lmax = 0;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    key[e] = doc0 + e < n_docs ? score_key(fv[e]) : 0u;
-    lmax = max(lmax, key[e]);
-  }
+  for (int e = 0; e < E; ++e) key[e] = (int)entry_doc(e, lane) < lim ? score_key(fv[e]) : 0u;
+  uint32_t lmax = 0, ldoc = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (key[e] > lmax) {
+      lmax = key[e];
+      ldoc = entry_doc(e, lane);
+    }
   for (int r = 0; r < m; ++r) {
     const uint32_t wm = wave_max_u32(lmax);
     if (wm == 0) {  // no valid entry left (tile smaller than m)
       if (lane == 0) out[r] = 0;
       continue;
     }
-    const int wl = (int)__builtin_ctzll(__ballot(lmax == wm));
-    if (lane == wl) {
-      int eb = 0;
-#pragma unroll
-      for (int e = E - 1; e >= 0; --e)
-        if (key[e] == wm) eb = e;
-      out[r] = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(doc0 + eb));
+    const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(lmax == wm ? 0xFFFFFFFFu - ldoc : 0u);
+    if (lane == ((doc >> 2) & 63u)) {
+      out[r] = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc));
+      const int eb = (int)(((doc >> 8) << 2) | (doc & 3u));
       lmax = 0;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         key[e] = e == eb ? 0u : key[e];
-        lmax = max(lmax, key[e]);
+        if (key[e] > lmax) {
+          lmax = key[e];
+          ldoc = entry_doc(e, lane);
+        }
       }
     }
   }
@@ -281,35 +293,39 @@ __device__ __forceinline__ void emit_above(const float (&fv)[(1 << S) / 64], int
                                            uint64_t* __restrict__ list, int32_t* __restrict__ cnt,
                                            int32_t C) {
   constexpr int E = (1 << S) / 64;
-  const int lane = lane_id();
+  const uint32_t lane = lane_id();
   const float th = key_score((uint32_t)(theta >> 32));
-  const uint32_t th_doc = 0xFFFFFFFFu - (uint32_t)theta;
-  const int64_t doc0 = (tile << S) + (int64_t)lane * E;
-  const int64_t lim_hi = n_docs - doc0;            // entries e >= lim_hi are past n_docs
-  const int64_t lim_tie = (int64_t)th_doc - doc0;  // ties pass for e < lim_tie
+  const int64_t base = tile << S;
+  constexpr int64_t D = 1 << S;
+  // tile-local bounds, clamped to [-1, D]: docs >= lim are past n_docs, ties
+  // pass for docs < tie
+  const int lim = (int)max<int64_t>(-1, min<int64_t>(D, n_docs - base));
+  const int tie = (int)max<int64_t>(
+      -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base));
   float mx = fv[0];
 #pragma unroll
   for (int e = 1; e < E; ++e) mx = fmaxf(mx, fv[e]);
   int c = 0;
-  if (!(mx < th && lim_hi >= E)) {
+  if (!(mx < th && lim == D)) {
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-      c += (e < lim_hi) & ((fv[e] > th) | ((fv[e] == th) & (e < lim_tie)));
+    for (int e = 0; e < E; ++e) {
+      const int d = (int)entry_doc(e, lane);
+      c += (d < lim) & ((fv[e] > th) | ((fv[e] == th) & (d < tie)));
+    }
   }
   if (__ballot(c > 0) == 0) return;  // common: nothing of this tile passes
   const uint32_t incl = wave_incl_scan((uint32_t)c);
-  int base = 0;
-  if (lane == 63) base = atomicAdd(cnt, (int)incl);
-  base = __shfl(base, 63, 64);
-  int pos = base + (int)incl - c;
+  int pos = 0;
+  if (lane == 63) pos = atomicAdd(cnt, (int)incl);
+  pos = __shfl(pos, 63, 64) + (int)incl - c;
   if (c == 0) return;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const bool pass = (e < lim_hi) & ((fv[e] > th) | ((fv[e] == th) & (e < lim_tie)));
+    const int d = (int)entry_doc(e, lane);
+    const bool pass = (d < lim) & ((fv[e] > th) | ((fv[e] == th) & (d < tie)));
     if (pass) {
       if (pos < C)
-        list[pos] = ((uint64_t)score_key(fv[e]) << 32) |
-                    (uint64_t)(0xFFFFFFFFu - (uint32_t)(doc0 + e));
+        list[pos] = ((uint64_t)score_key(fv[e]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + d));
       ++pos;
     }
   }
@@ -348,11 +364,21 @@ __device__ __forceinline__ Desc load_desc(const IndexArgs& a, int32_t term, int6
   return d;
 }
 
+// Inclusive prefix sum inside 16-lane rows (DPP row_shr; enough for T <= 16
+// because lanes >= T hold 0).
+__device__ __forceinline__ uint32_t scan16(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  return x;
+}
+
 // An item's posting rows: each query term's segment is cut into rows of 64
-// postings (one per lane), so a row belongs to one term and its adds need no
-// term mask.  Lane j of the table describes row j0 + j of the item.
+// postings (one per lane), so a row belongs to one term and needs no term
+// mask.  Lane j of the table describes row j0 + j of the item.
 struct Rows {
-  int64_t base;    // posting index of the row's first posting
+  int64_t base;    // posting index of the row's first posting (0 past the end)
   uint32_t cnt;    // postings in the row (0: past the item's rows)
   uint32_t nrows;  // rows of the item (uniform)
 };
@@ -362,40 +388,58 @@ __device__ __forceinline__ Rows make_rows(const Desc& d, int T, uint32_t j0) {
   const uint32_t len = ((int)lane < T && d.ok) ? d.r1 - d.r0 : 0u;
   const int64_t beg = d.ip + (int64_t)d.r0;
   const uint32_t nr = (len + 63u) >> 6;
-  const uint32_t rincl = wave_incl_scan(nr);
+  const uint32_t rincl = T <= 16 ? scan16(nr) : wave_incl_scan(nr);
   Rows r;
   r.nrows = lane_u32(rincl, T - 1);
   const uint32_t j = j0 + lane;  // the row this lane describes
-  int64_t b = 0;
-  uint32_t rs = 0, l = 0;
-  for (int s = 0; s < T; ++s) {  // term of row j: rincl[s] - nr[s] <= j < rincl[s]
-    const uint32_t e = lane_u32(rincl, s), st = e - lane_u32(nr, s);
-    if (j >= st && j < e) {
-      b = lane_i64(beg, s);
-      rs = st;
-      l = lane_u32(len, s);
-    }
+  // its term s = #{s < T : rincl[s] <= j}, by binary lifting over ds_bpermute
+  int pos = 0;
+#pragma unroll
+  for (int step = 64; step >= 1; step >>= 1) {
+    if (step > T) continue;  // uniform
+    const int c = pos + step;
+    const uint32_t x = (uint32_t)__shfl((int)rincl, min(c, T) - 1, 64);
+    if (c <= T && x <= j) pos = c;
   }
-  const uint32_t k = j - rs;  // row index inside its term
-  r.base = b + 64 * (int64_t)k;
-  r.cnt = j < r.nrows ? min(64u, l - 64u * k) : 0u;
+  const uint32_t st = (uint32_t)__shfl((int)(rincl - nr), pos, 64);
+  const uint32_t l = (uint32_t)__shfl((int)len, pos, 64);
+  const uint32_t blo = (uint32_t)__shfl((int)(uint32_t)beg, pos, 64);
+  const uint32_t bhi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)beg >> 32), pos, 64);
+  const uint32_t k = j - st;  // row index inside its term
+  const bool in = j < r.nrows;
+  r.base = in ? (int64_t)(((uint64_t)bhi << 32) | blo) + 64 * (int64_t)k : 0;
+  r.cnt = in ? min(64u, l - 64u * k) : 0u;
+  return r;
+}
+
+// Buffer descriptors over the whole posting arrays (built once per kernel
+// from kernel arguments): a row's loads are then one scalar offset (its base)
+// plus the constant lane offset, with no per-lane address arithmetic.  Needs
+// (nnz + pad) * 4 < 2^32 (use_pipe checks it).
+struct PostingRsrc {
+  __amdgpu_buffer_rsrc_t ldoc, val;
+};
+
+__device__ __forceinline__ PostingRsrc posting_rsrc(const IndexArgs& a) {
+  PostingRsrc r;
+  r.ldoc = __builtin_amdgcn_make_buffer_rsrc((void*)a.ldoc, 0, 0x7FFFFFFF, 0x00020000);
+  r.val = __builtin_amdgcn_make_buffer_rsrc((void*)a.val, 0, 0x7FFFFFFF, 0x00020000);
   return r;
 }
 
 // Loads of table rows [j0, j0 + kJ): slot + score per lane.  Lanes past a
-// row's postings read the pad posting of their lane (slot = lane, score
-// +0.0): adding +0.0 leaves any accumulator's bits unchanged (an accumulator
-// is never -0.0), so the adds need no mask either.
-__device__ __forceinline__ void issue_rows(const IndexArgs& a, const Rows& R, int j0,
+// row's postings read the next postings (or the zeroed pad after the last
+// one) and are masked by add_rows.  Every load is issued, so the vmcnt waits
+// stay counted.
+__device__ __forceinline__ void issue_rows(const PostingRsrc& pr, const Rows& R, int j0,
                                            uint32_t (&ld)[kJ], float (&v)[kJ]) {
   const uint32_t lane = lane_id();
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
-    const int64_t base = lane_i64(R.base, j0 + j);
-    const uint32_t cnt = lane_u32(R.cnt, j0 + j);
-    const int64_t g = lane < cnt ? base + lane : a.pad + lane;
-    ld[j] = a.ldoc[g];
-    v[j] = a.val[g];
+    const uint32_t base = lane_u32((uint32_t)R.base, j0 + j);
+    ld[j] = __builtin_amdgcn_raw_buffer_load_b16(pr.ldoc, (int)(lane * 2u), (int)(base * 2u), 0);
+    v[j] = __uint_as_float(
+        __builtin_amdgcn_raw_buffer_load_b32(pr.val, (int)(lane * 4u), (int)(base * 4u), 0));
   }
 }
 
@@ -404,26 +448,26 @@ __device__ __forceinline__ void issue_rows(const IndexArgs& a, const Rows& R, in
 // executes a wave's instructions in order, so row j+1's read sees row j's
 // write.  (An LDS float atomic does the same add at ~2.5x the cost on
 // gfx950: 23.8 vs 10.9 ms for the config-3 score pass, BM25_ABLATE=8.)
-__device__ __forceinline__ void add_rows(float* acc, const uint32_t (&ld)[kJ], const float (&v)[kJ],
+__device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0,
+                                         const uint32_t (&ld)[kJ], const float (&v)[kJ],
                                          uint32_t n, int mode) {
+  const uint32_t lane = lane_id();
   if (mode & 1) {  // ablation: consume the loads, no adds
 #pragma unroll
     for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
     return;
   }
-  if (mode & 8) {  // ablation: LDS float atomics
 #pragma unroll
-    for (int j = 0; j < kJ; ++j)
-      if ((uint32_t)j < n) lds_add(acc + ld[j], v[j]);
-    return;
+  for (int j = 0; j < kJ; ++j) {
+    if ((uint32_t)j < n && lane < lane_u32(R.cnt, j0 + j)) {
+      if (mode & 8) lds_add(acc + ld[j], v[j]);  // ablation: LDS float atomics
+      else acc[ld[j]] = acc[ld[j]] + v[j];
+    }
   }
-#pragma unroll
-  for (int j = 0; j < kJ; ++j)
-    if ((uint32_t)j < n) acc[ld[j]] = acc[ld[j]] + v[j];
 }
 
 struct Cursor {  // item it0 + n*stride as (ti, qi)
-  int64_t ti, qi;
+  int32_t ti, qi;
 };
 
 // ---------------------------------------------------------------------------
@@ -489,25 +533,26 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   __shared__ __attribute__((aligned(16))) float acc_all[kWaves * D];
   const int wave = uniform((int)(threadIdx.x >> 6));
   float* acc = acc_all + wave * D;
-  const int64_t nq = sg.nq_dev ? (int64_t)*sg.nq_dev : (int64_t)sg.nq_host;
+  const int32_t nq = sg.nq_dev ? *sg.nq_dev : sg.nq_host;
   const int P = sg.P;
-  const int64_t nS = (a.ntiles + P - 1) / P;
-  const int64_t nt = PH == kAll ? a.ntiles : (PH == kSample ? nS : a.ntiles - nS);
-  const int64_t nitems = nt * nq;
+  const int32_t nS = (int32_t)((a.ntiles + P - 1) / P);
+  const int32_t nt = PH == kAll ? (int32_t)a.ntiles : (PH == kSample ? nS : (int32_t)a.ntiles - nS);
+  const int64_t nitems = (int64_t)nt * nq;
   const int64_t per = (nitems + 7) >> 3;
   const int64_t grp = blockIdx.x & 7;
   const int64_t lo = grp * per;
   const int64_t hi = min(nitems, lo + per);
-  const int64_t stride = (int64_t)(gridDim.x >> 3) * kWaves;
+  const int32_t stride = (int32_t)(gridDim.x >> 3) * kWaves;
   const int64_t it0 = lo + (int64_t)(blockIdx.x >> 3) * kWaves + wave;
   if (it0 >= hi) return;  // wave-uniform; no barriers in this kernel
-  const int64_t count = (hi - it0 + stride - 1) / stride;
-  const int64_t sdiv = stride / nq, smod = stride - sdiv * nq;
+  const int32_t count = (int32_t)((hi - it0 + stride - 1) / stride);
+  const int32_t sdiv = stride / nq, smod = stride - sdiv * nq;
   const int tl = min(lane_id(), T - 1);
+  const PostingRsrc pr = posting_rsrc(a);
 
   // cursor of item n+1 from item n's (stays on the last item past the end,
   // so every stage keeps loading valid addresses)
-  auto next = [&](Cursor c, int64_t n) -> Cursor {
+  auto next = [&](Cursor c, int32_t n) -> Cursor {
     if (n + 1 < count) {
       c.ti += sdiv;
       c.qi += smod;
@@ -519,27 +564,25 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     return c;
   };
   auto terms_of = [&](const Cursor& c) -> int32_t {
-    const int64_t q = sg.qmap ? (int64_t)sg.qmap[c.qi] : c.qi;
-    return queries[q * T + tl];
+    const int32_t q = sg.qmap ? sg.qmap[c.qi] : c.qi;
+    return queries[(int64_t)q * T + tl];
   };
 
   zero_acc<S>(acc);
   Cursor cD;
-  cD.ti = it0 / nq;
-  cD.qi = it0 - cD.ti * nq;
+  cD.ti = (int32_t)(it0 / nq);
+  cD.qi = (int32_t)(it0 - (int64_t)cD.ti * nq);
   Cursor cC = next(cD, 0), cB = next(cC, 1), cA = next(cB, 2);
   // prologue: item 0's first rows, item 1's bounds, item 2's terms
-  const int32_t tm0 = terms_of(cD), tm1 = terms_of(cC);
-  int32_t tmB = terms_of(cB);
-  Desc dD = load_desc(a, tm0, tile_of<PH>(cD.ti, P));
-  Desc dC = load_desc(a, tm1, tile_of<PH>(cC.ti, P));
-  Rows rD = make_rows(dD, T, 0);
+  int32_t tmD = terms_of(cD), tmC = terms_of(cC), tmB = terms_of(cB);
+  Desc dC = load_desc(a, tmC, tile_of<PH>(cC.ti, P));
+  Rows rD = make_rows(load_desc(a, tmD, tile_of<PH>(cD.ti, P)), T, 0);
   uint32_t ltD[kJ];
   float vD[kJ];
-  issue_rows(a, rD, 0, ltD, vD);
+  issue_rows(pr, rD, 0, ltD, vD);
   uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
 
-  for (int64_t n = 0; n < count; ++n) {
+  for (int32_t n = 0; n < count; ++n) {
     // (1) terms of item n+3, (2) bounds of item n+2
     const int32_t tmA = terms_of(cA);
     const Desc dB = load_desc(a, tmB, tile_of<PH>(cB.ti, P));
@@ -548,24 +591,25 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     const uint32_t nrD = rD.nrows;
     uint32_t ltX[kJ];
     float vX[kJ];
-    if (nrD > kJ) issue_rows(a, rD, kJ, ltX, vX);
+    if (nrD > kJ) issue_rows(pr, rD, kJ, ltX, vX);
     const Rows rC = make_rows(dC, T, 0);
     uint32_t ltC[kJ];
     float vC[kJ];
-    issue_rows(a, rC, 0, ltC, vC);
+    issue_rows(pr, rC, 0, ltC, vC);
     const uint64_t thC = PH == kRest ? theta[cC.qi] : 0ull;
     // (4) item n: adds in row order, then selection
     const int64_t tile = tile_of<PH>(cD.ti, P);
-    add_rows(acc, ltD, vD, min(nrD, (uint32_t)kJ), mode);
-    if (nrD > kJ) add_rows(acc, ltX, vX, min(nrD - kJ, (uint32_t)kJ), mode);
+    add_rows(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ), mode);
+    if (nrD > kJ) add_rows(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ), mode);
     if (nrD > 2 * kJ) {  // heavy item: the remaining rows, block by block
+      const Desc dD = load_desc(a, tmD, tile);
       Rows t = rD;
       for (uint32_t j = 2 * kJ; j < nrD; j += kJ) {
         if ((j & 63) == 0) t = make_rows(dD, T, j);
         uint32_t ltY[kJ];
         float vY[kJ];
-        issue_rows(a, t, (int)(j & 63), ltY, vY);
-        add_rows(acc, ltY, vY, min(nrD - j, (uint32_t)kJ), mode);
+        issue_rows(pr, t, (int)(j & 63), ltY, vY);
+        add_rows(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ), mode);
       }
     }
     float fv[D / 64];
@@ -573,17 +617,18 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     if (mode & 4) {  // ablation: no selection
       if (fv[0] == 12345.f) cand[0] = 0;
     } else if (PH == kRest) {
-      emit_above<S>(fv, tile, a.n_docs, thD, list + cD.qi * C, list_cnt + cD.qi, C);
+      emit_above<S>(fv, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
     } else {
-      select_top<S>(fv, tile, a.n_docs, kTileM, cand + (cD.qi * nt + cD.ti) * kTileM);
+      select_top<S>(fv, tile, a.n_docs, kTileM, cand + ((int64_t)cD.qi * nt + cD.ti) * kTileM);
     }
     // rotate the pipeline
     cD = cC;
     cC = cB;
     cB = cA;
     cA = next(cA, n + 3);
+    tmD = tmC;
+    tmC = tmB;
     tmB = tmA;
-    dD = dC;
     dC = dB;
     rD = rC;
     thD = thC;
@@ -647,7 +692,7 @@ __global__ __launch_bounds__(kRescoreNT) void rescore_kernel(IndexArgs a,
     __syncthreads();
     for (int i = threadIdx.x; i < D; i += blockDim.x) {
       const int64_t doc = (tile << S) + i;
-      keys[i] = doc < a.n_docs ? make_key(acc[acc_slot((uint32_t)i, S)], (uint32_t)doc) : 0ull;
+      keys[i] = doc < a.n_docs ? make_key(acc[i], (uint32_t)doc) : 0ull;
     }
     __syncthreads();
     bitonic_sort_desc(keys, D);
@@ -668,16 +713,17 @@ __global__ __launch_bounds__(64) void scores_dense_kernel(IndexArgs a,
   add_item<S>(a, tile, query, T, acc);
   float fv[E];
   take_entries<S>(acc, fv);
-  const int64_t d0 = (tile << S) + (int64_t)lane_id() * E;  // this lane's E docs
-  if (d0 + E <= a.n_docs) {
-    float4* o4 = reinterpret_cast<float4*>(out + d0);
+  const int64_t base = tile << S;
+  const uint32_t lane = lane_id();
+  if (base + D <= a.n_docs) {
 #pragma unroll
-    for (int j = 0; j < E / 4; ++j)
-      o4[j] = make_float4(fv[4 * j], fv[4 * j + 1], fv[4 * j + 2], fv[4 * j + 3]);
+    for (int j = 0; j < E / 4; ++j)  // docs base + 256 j + 4 lane + (0..3)
+      *reinterpret_cast<float4*>(out + base + entry_doc(4 * j, lane)) =
+          make_float4(fv[4 * j], fv[4 * j + 1], fv[4 * j + 2], fv[4 * j + 3]);
   } else {
 #pragma unroll
     for (int e = 0; e < E; ++e)
-      if (d0 + e < a.n_docs) out[d0 + e] = fv[e];
+      if (base + entry_doc(e, lane) < a.n_docs) out[base + entry_doc(e, lane)] = fv[e];
   }
 }
 
@@ -707,7 +753,7 @@ __global__ __launch_bounds__(256) void build_tables_kernel(
       const int32_t dp = p > a0 ? indices[p - 1] : -1;
       const bool ok = d >= 0 && (int64_t)d < n_docs && d > dp;
       if (!ok) atomicOr(err, 1);
-      ldoc[p] = (uint16_t)acc_slot((uint32_t)d & mask, S);
+      ldoc[p] = (uint16_t)((uint32_t)d & mask);  // tile-local doc = LDS slot
       if (heavy && ok) {
         const int64_t tp = dp >= 0 ? ((int64_t)dp >> S) : -1;
         const int64_t tc = (int64_t)d >> S;
@@ -993,15 +1039,16 @@ static int persistent_grid(K kernel) {
 
 // The pipelined kernel serves queries of 1..64 terms (BM25_NO_PIPE=1 forces
 // the plain one, which also serves longer queries).
-static bool use_pipe(int64_t T) {
+static bool use_pipe(const DevIndex& ix, int64_t T) {
   static const bool off = getenv("BM25_NO_PIPE") != nullptr;
-  return !off && T >= 1 && T <= kGroup;
+  return !off && T >= 1 && T <= kGroup && (ix.nnz + kPostingPad) * 4 < 0x7FFFFFFF &&
+         ix.ntiles * 4096 < 0x7FFFFFFF;
 }
 
 template <int S, int PH>
 static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
                         const Workspace& ws, hipStream_t st) {
-  if (use_pipe(T)) {
+  if (use_pipe(ix, T)) {
     static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH>);
     static const int mode = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
     hipLaunchKernelGGL((score_pipe_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0,
