@@ -415,15 +415,16 @@ __device__ __forceinline__ Rows make_rows(const Desc& d, int T, uint32_t j0) {
 // Buffer descriptors over the whole posting arrays (built once per kernel
 // from kernel arguments): a row's loads are then one scalar offset (its base)
 // plus the constant lane offset, with no per-lane address arithmetic.  Needs
-// (nnz + pad) * 4 < 2^32 (use_pipe checks it).
+// (nnz + pad) * 4 < 2^32 bytes (use_pipe checks it; larger indices take the
+// plain kernel).
 struct PostingRsrc {
   __amdgpu_buffer_rsrc_t ldoc, val;
 };
 
 __device__ __forceinline__ PostingRsrc posting_rsrc(const IndexArgs& a) {
   PostingRsrc r;
-  r.ldoc = __builtin_amdgcn_make_buffer_rsrc((void*)a.ldoc, 0, 0x7FFFFFFF, 0x00020000);
-  r.val = __builtin_amdgcn_make_buffer_rsrc((void*)a.val, 0, 0x7FFFFFFF, 0x00020000);
+  r.ldoc = __builtin_amdgcn_make_buffer_rsrc((void*)a.ldoc, 0, -1, 0x00020000);  // 2^32-1 bytes
+  r.val = __builtin_amdgcn_make_buffer_rsrc((void*)a.val, 0, -1, 0x00020000);
   return r;
 }
 
@@ -1041,8 +1042,7 @@ static int persistent_grid(K kernel) {
 // the plain one, which also serves longer queries).
 static bool use_pipe(const DevIndex& ix, int64_t T) {
   static const bool off = getenv("BM25_NO_PIPE") != nullptr;
-  return !off && T >= 1 && T <= kGroup && (ix.nnz + kPostingPad) * 4 < 0x7FFFFFFF &&
-         ix.ntiles * 4096 < 0x7FFFFFFF;
+  return !off && T >= 1 && T <= kGroup && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
 }
 
 template <int S, int PH>
