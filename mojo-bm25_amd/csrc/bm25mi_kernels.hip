@@ -467,9 +467,11 @@ __device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0,
   }
 }
 
-struct Cursor {  // item it0 + n*stride as (ti, qi)
-  int32_t ti, qi;
+struct Cursor {  // group item rit = (ti, qi)
+  int32_t rit, ti, qi;
 };
+
+constexpr int kChunk = 4;  // items per claim of the dynamic item distribution
 
 // ---------------------------------------------------------------------------
 // Persistent score kernel: kWaves independent waves per workgroup, each with a
@@ -529,7 +531,7 @@ template <int S, int PH>
 __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t T, Stage sg,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
-    int32_t* __restrict__ list_cnt, int32_t C, int mode) {
+    int32_t* __restrict__ list_cnt, int32_t C, int32_t* __restrict__ wctr, int mode) {
   constexpr int D = 1 << S;
   __shared__ __attribute__((aligned(16))) float acc_all[kWaves * D];
   const int wave = uniform((int)(threadIdx.x >> 6));
@@ -540,40 +542,56 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   const int32_t nt = PH == kAll ? (int32_t)a.ntiles : (PH == kSample ? nS : (int32_t)a.ntiles - nS);
   const int64_t nitems = (int64_t)nt * nq;
   const int64_t per = (nitems + 7) >> 3;
-  const int64_t grp = blockIdx.x & 7;
+  const int grp = blockIdx.x & 7;
   const int64_t lo = grp * per;
-  const int64_t hi = min(nitems, lo + per);
-  const int32_t stride = (int32_t)(gridDim.x >> 3) * kWaves;
-  const int64_t it0 = lo + (int64_t)(blockIdx.x >> 3) * kWaves + wave;
-  if (it0 >= hi) return;  // wave-uniform; no barriers in this kernel
-  const int32_t count = (int32_t)((hi - it0 + stride - 1) / stride);
-  const int32_t sdiv = stride / nq, smod = stride - sdiv * nq;
+  const int32_t ngi = (int32_t)max<int64_t>(0, min(nitems, lo + per) - lo);  // the group's items
+  if (ngi == 0) return;
+  int32_t* ctr = wctr + grp;
   const int tl = min(lane_id(), T - 1);
   const PostingRsrc pr = posting_rsrc(a);
 
-  // cursor of item n+1 from item n's (stays on the last item past the end,
-  // so every stage keeps loading valid addresses)
-  auto next = [&](Cursor c, int32_t n) -> Cursor {
-    if (n + 1 < count) {
-      c.ti += sdiv;
-      c.qi += smod;
-      if (c.qi >= nq) {
-        c.qi -= nq;
+  // Items are claimed kChunk at a time from the group's counter, in order, so
+  // the waves of an XCD always work on the same few tiles (L2 reuse of their
+  // posting segments across queries).  A claim is issued one chunk ahead and
+  // its result read only when the cursor reaches that chunk.
+  auto claim = [&]() -> int32_t {
+    int32_t v = 0;
+    if (lane_id() == 0) v = atomicAdd(ctr, kChunk);
+    return v;  // lane 0 holds the claimed chunk start (VGPR: read lazily)
+  };
+  int32_t pending = claim();
+  auto at = [&](int32_t rit) -> Cursor {  // cursor of group item rit (0,0 past the end)
+    Cursor c;
+    c.rit = rit;
+    const int64_t it = lo + min(rit, ngi - 1);
+    c.ti = (int32_t)(it / nq);
+    c.qi = (int32_t)(it - (int64_t)c.ti * nq);
+    return c;
+  };
+  auto next = [&](Cursor c) -> Cursor {
+    if (c.rit >= ngi) return c;  // exhausted: stay
+    if (((c.rit + 1) % kChunk) != 0 && c.rit + 1 < ngi) {
+      ++c.rit;
+      if (++c.qi == nq) {
+        c.qi = 0;
         ++c.ti;
       }
+      return c;
     }
-    return c;
+    const int32_t b = uniform(pending);
+    pending = claim();
+    return at(b);
   };
   auto terms_of = [&](const Cursor& c) -> int32_t {
     const int32_t q = sg.qmap ? sg.qmap[c.qi] : c.qi;
     return queries[(int64_t)q * T + tl];
   };
 
+  Cursor cD = at(uniform(pending));
+  pending = claim();
+  if (cD.rit >= ngi) return;
   zero_acc<S>(acc);
-  Cursor cD;
-  cD.ti = (int32_t)(it0 / nq);
-  cD.qi = (int32_t)(it0 - (int64_t)cD.ti * nq);
-  Cursor cC = next(cD, 0), cB = next(cC, 1), cA = next(cB, 2);
+  Cursor cC = next(cD), cB = next(cC), cA = next(cB);
   // prologue: item 0's first rows, item 1's bounds, item 2's terms
   int32_t tmD = terms_of(cD), tmC = terms_of(cC), tmB = terms_of(cB);
   Desc dC = load_desc(a, tmC, tile_of<PH>(cC.ti, P));
@@ -583,7 +601,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   issue_rows(pr, rD, 0, ltD, vD);
   uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
 
-  for (int32_t n = 0; n < count; ++n) {
+  while (cD.rit < ngi) {
     // (1) terms of item n+3, (2) bounds of item n+2
     const int32_t tmA = terms_of(cA);
     const Desc dB = load_desc(a, tmB, tile_of<PH>(cB.ti, P));
@@ -626,7 +644,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     cD = cC;
     cC = cB;
     cB = cA;
-    cA = next(cA, n + 3);
+    cA = next(cA);
     tmD = tmC;
     tmC = tmB;
     tmB = tmA;
@@ -1051,9 +1069,11 @@ static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const S
   if (use_pipe(ix, T)) {
     static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH>);
     static const int mode = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
+    int32_t* wctr = ws.wctr + 8 * (sg.qmap ? 2 : (PH == kRest ? 1 : 0));
+    hipMemsetAsync(wctr, 0, 8 * sizeof(int32_t), st);
     hipLaunchKernelGGL((score_pipe_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0,
                        st, args_of(ix), q, (int32_t)T, sg, ws.theta, ws.cand, ws.list,
-                       ws.list_cnt, ws.list_cap, mode);
+                       ws.list_cnt, ws.list_cap, wctr, mode);
     return;
   }
   static const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
