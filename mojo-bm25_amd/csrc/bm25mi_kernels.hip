@@ -471,7 +471,36 @@ struct Cursor {  // group item rit = (ti, qi)
   int32_t rit, ti, qi;
 };
 
-constexpr int kChunk = 4;  // items per claim of the dynamic item distribution
+// Item claims of the pipelined kernel: lane 0 adds 1 to the group counter.
+// hipcc would wait for the returned value right after the atomic (draining
+// every load in flight), so the atomic is inline asm and its value is read by
+// claim_read one iteration later, after `s_waitcnt vmcnt(12)`: by then at
+// least 20 loads were issued after the atomic (1 term + 3 bound loads + 16
+// row loads per iteration), so the atomic (and the oldest of those loads) has
+// completed while the newest stay in flight.
+__device__ __forceinline__ uint32_t claim_issue(int32_t* ctr) {
+  uint32_t v;
+  uint64_t saved;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "global_atomic_add %0, %2, %3, off sc0\n\t"
+      "s_mov_b64 exec, %1"
+      : "=&v"(v), "=&s"(saved)
+      : "v"(ctr), "v"(1u)
+      : "memory");
+  return v;
+}
+__device__ __forceinline__ int32_t claim_read(uint32_t v) {
+  int32_t r;
+  asm volatile("s_waitcnt vmcnt(12)\n\tv_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v) : "memory");
+  return r;
+}
+__device__ __forceinline__ int32_t claim_read_now(uint32_t v) {
+  int32_t r;
+  asm volatile("s_waitcnt vmcnt(0)\n\tv_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v) : "memory");
+  return r;
+}
 
 // ---------------------------------------------------------------------------
 // Persistent score kernel: kWaves independent waves per workgroup, each with a
@@ -550,17 +579,13 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   const int tl = min(lane_id(), T - 1);
   const PostingRsrc pr = posting_rsrc(a);
 
-  // Items are claimed kChunk at a time from the group's counter, in order, so
+  // Items are claimed one at a time from the group's counter, in order, so
   // the waves of an XCD always work on the same few tiles (L2 reuse of their
-  // posting segments across queries).  A claim is issued one chunk ahead and
-  // its result read only when the cursor reaches that chunk.
-  auto claim = [&]() -> int32_t {
-    int32_t v = 0;
-    if (lane_id() == 0) v = atomicAdd(ctr, kChunk);
-    return v;  // lane 0 holds the claimed chunk start (VGPR: read lazily)
-  };
-  int32_t pending = claim();
-  auto at = [&](int32_t rit) -> Cursor {  // cursor of group item rit (0,0 past the end)
+  // posting segments across queries).  Each iteration issues the claim of the
+  // item it starts next time and reads the previous claim (claim_issue /
+  // claim_read: the wait is counted, behind this iteration's loads).
+  auto claim = [&]() -> uint32_t { return claim_issue(ctr); };
+  auto at = [&](int32_t rit) -> Cursor {  // cursor of group item rit (clamped past the end)
     Cursor c;
     c.rit = rit;
     const int64_t it = lo + min(rit, ngi - 1);
@@ -568,30 +593,17 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     c.qi = (int32_t)(it - (int64_t)c.ti * nq);
     return c;
   };
-  auto next = [&](Cursor c) -> Cursor {
-    if (c.rit >= ngi) return c;  // exhausted: stay
-    if (((c.rit + 1) % kChunk) != 0 && c.rit + 1 < ngi) {
-      ++c.rit;
-      if (++c.qi == nq) {
-        c.qi = 0;
-        ++c.ti;
-      }
-      return c;
-    }
-    const int32_t b = uniform(pending);
-    pending = claim();
-    return at(b);
-  };
   auto terms_of = [&](const Cursor& c) -> int32_t {
     const int32_t q = sg.qmap ? sg.qmap[c.qi] : c.qi;
     return queries[(int64_t)q * T + tl];
   };
 
-  Cursor cD = at(uniform(pending));
-  pending = claim();
+  Cursor cD = at(claim_read_now(claim()));
   if (cD.rit >= ngi) return;
+  Cursor cC = at(claim_read_now(claim()));
+  Cursor cB = at(claim_read_now(claim()));
+  uint32_t pending = claim();
   zero_acc<S>(acc);
-  Cursor cC = next(cD), cB = next(cC), cA = next(cB);
   // prologue: item 0's first rows, item 1's bounds, item 2's terms
   int32_t tmD = terms_of(cD), tmC = terms_of(cC), tmB = terms_of(cB);
   Desc dC = load_desc(a, tmC, tile_of<PH>(cC.ti, P));
@@ -602,7 +614,9 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
 
   while (cD.rit < ngi) {
-    // (1) terms of item n+3, (2) bounds of item n+2
+    // (0) claim item n+4, (1) terms of item n+3, (2) bounds of item n+2
+    const Cursor cA = at(claim_read(pending));
+    pending = claim();
     const int32_t tmA = terms_of(cA);
     const Desc dB = load_desc(a, tmB, tile_of<PH>(cB.ti, P));
     // (3) item n's second row block (issued before item n+1's rows so that
@@ -644,7 +658,6 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     cD = cC;
     cC = cB;
     cB = cA;
-    cA = next(cA);
     tmD = tmC;
     tmC = tmB;
     tmB = tmA;
