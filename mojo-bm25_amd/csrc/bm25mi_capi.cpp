@@ -88,7 +88,6 @@ void free_ws(Workspace& ws) {
   hipFree(ws.nflag);
   hipFree(ws.queue);
   hipFree(ws.counters);
-  hipFree(ws.wctr);
   ws = Workspace{};
 }
 
@@ -121,7 +120,6 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMalloc(&ws.nflag, sizeof(int32_t) * q), "hipMalloc(nflag)");
   HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
   HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
-  HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * 24), "hipMalloc(wctr)");
   HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * 4), "hipMemset(counters)");
   ws.list_cap = C;
   ws.cap_q = q;

@@ -72,8 +72,6 @@ struct Workspace {
   int32_t* queue = nullptr;      // [Q*maxflag] items = qi*maxflag + i
   int32_t* counters = nullptr;   // [0]/[1] rescore queue length / pop cursor,
                                  // [2] fallback queries, [3] tiles re-scored this search
-  int32_t* wctr = nullptr;       // [3][8] per-XCD-group item counters of the score
-                                 // kernels (sample, rest, fallback)
 };
 
 // Flag slots per query: a flagged tile holds kTileM keys of the top-(k-1), so

@@ -27,7 +27,9 @@
 // score vector, with untouched documents scoring 0.
 #include "bm25mi_internal.h"
 
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 namespace bm25mi {
 
@@ -467,40 +469,9 @@ __device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0,
   }
 }
 
-struct Cursor {  // group item rit = (ti, qi)
-  int32_t rit, ti, qi;
+struct Cursor {  // item it0 + n*stride as (ti, qi)
+  int32_t ti, qi;
 };
-
-// Item claims of the pipelined kernel: lane 0 adds 1 to the group counter.
-// hipcc would wait for the returned value right after the atomic (draining
-// every load in flight), so the atomic is inline asm and its value is read by
-// claim_read one iteration later, after `s_waitcnt vmcnt(12)`: by then at
-// least 20 loads were issued after the atomic (1 term + 3 bound loads + 16
-// row loads per iteration), so the atomic (and the oldest of those loads) has
-// completed while the newest stay in flight.
-__device__ __forceinline__ uint32_t claim_issue(int32_t* ctr) {
-  uint32_t v;
-  uint64_t saved;
-  asm volatile(
-      "s_mov_b64 %1, exec\n\t"
-      "s_mov_b64 exec, 1\n\t"
-      "global_atomic_add %0, %2, %3, off sc0\n\t"
-      "s_mov_b64 exec, %1"
-      : "=&v"(v), "=&s"(saved)
-      : "v"(ctr), "v"(1u)
-      : "memory");
-  return v;
-}
-__device__ __forceinline__ int32_t claim_read(uint32_t v) {
-  int32_t r;
-  asm volatile("s_waitcnt vmcnt(12)\n\tv_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v) : "memory");
-  return r;
-}
-__device__ __forceinline__ int32_t claim_read_now(uint32_t v) {
-  int32_t r;
-  asm volatile("s_waitcnt vmcnt(0)\n\tv_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v) : "memory");
-  return r;
-}
 
 // ---------------------------------------------------------------------------
 // Persistent score kernel: kWaves independent waves per workgroup, each with a
@@ -560,37 +531,51 @@ template <int S, int PH>
 __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t T, Stage sg,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
-    int32_t* __restrict__ list_cnt, int32_t C, int32_t* __restrict__ wctr, int mode) {
+    int32_t* __restrict__ list_cnt, int32_t C, int mode, uint64_t* __restrict__ stamps) {
   constexpr int D = 1 << S;
   __shared__ __attribute__((aligned(16))) float acc_all[kWaves * D];
   const int wave = uniform((int)(threadIdx.x >> 6));
   float* acc = acc_all + wave * D;
+  // diagnostic build only (BM25_ABLATE & 32): cycles per loop segment
+  uint64_t seg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = 0;
+#define BM25_STAMP(k)                                                           \
+  if (stamps) {                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    uint64_t t_;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    seg[k] += t_ - t_last;                                                      \
+    t_last = t_;                                                                \
+  }
+  BM25_STAMP(7);
   const int32_t nq = sg.nq_dev ? *sg.nq_dev : sg.nq_host;
   const int P = sg.P;
   const int32_t nS = (int32_t)((a.ntiles + P - 1) / P);
   const int32_t nt = PH == kAll ? (int32_t)a.ntiles : (PH == kSample ? nS : (int32_t)a.ntiles - nS);
   const int64_t nitems = (int64_t)nt * nq;
   const int64_t per = (nitems + 7) >> 3;
-  const int grp = blockIdx.x & 7;
+  const int64_t grp = blockIdx.x & 7;
   const int64_t lo = grp * per;
-  const int32_t ngi = (int32_t)max<int64_t>(0, min(nitems, lo + per) - lo);  // the group's items
-  if (ngi == 0) return;
-  int32_t* ctr = wctr + grp;
+  const int64_t hi = min(nitems, lo + per);
+  const int32_t stride = (int32_t)(gridDim.x >> 3) * kWaves;
+  const int64_t it0 = lo + (int64_t)(blockIdx.x >> 3) * kWaves + wave;
+  if (it0 >= hi) return;  // wave-uniform; no barriers in this kernel
+  const int32_t count = (int32_t)((hi - it0 + stride - 1) / stride);
+  const int32_t sdiv = stride / nq, smod = stride - sdiv * nq;
   const int tl = min(lane_id(), T - 1);
   const PostingRsrc pr = posting_rsrc(a);
 
-  // Items are claimed one at a time from the group's counter, in order, so
-  // the waves of an XCD always work on the same few tiles (L2 reuse of their
-  // posting segments across queries).  Each iteration issues the claim of the
-  // item it starts next time and reads the previous claim (claim_issue /
-  // claim_read: the wait is counted, behind this iteration's loads).
-  auto claim = [&]() -> uint32_t { return claim_issue(ctr); };
-  auto at = [&](int32_t rit) -> Cursor {  // cursor of group item rit (clamped past the end)
-    Cursor c;
-    c.rit = rit;
-    const int64_t it = lo + min(rit, ngi - 1);
-    c.ti = (int32_t)(it / nq);
-    c.qi = (int32_t)(it - (int64_t)c.ti * nq);
+  // cursor of item n+1 from item n's (stays on the last item past the end,
+  // so every stage keeps loading valid addresses)
+  auto next = [&](Cursor c, int32_t n) -> Cursor {
+    if (n + 1 < count) {
+      c.ti += sdiv;
+      c.qi += smod;
+      if (c.qi >= nq) {
+        c.qi -= nq;
+        ++c.ti;
+      }
+    }
     return c;
   };
   auto terms_of = [&](const Cursor& c) -> int32_t {
@@ -598,12 +583,11 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     return queries[(int64_t)q * T + tl];
   };
 
-  Cursor cD = at(claim_read_now(claim()));
-  if (cD.rit >= ngi) return;
-  Cursor cC = at(claim_read_now(claim()));
-  Cursor cB = at(claim_read_now(claim()));
-  uint32_t pending = claim();
   zero_acc<S>(acc);
+  Cursor cD;
+  cD.ti = (int32_t)(it0 / nq);
+  cD.qi = (int32_t)(it0 - (int64_t)cD.ti * nq);
+  Cursor cC = next(cD, 0), cB = next(cC, 1), cA = next(cB, 2);
   // prologue: item 0's first rows, item 1's bounds, item 2's terms
   int32_t tmD = terms_of(cD), tmC = terms_of(cC), tmB = terms_of(cB);
   Desc dC = load_desc(a, tmC, tile_of<PH>(cC.ti, P));
@@ -612,13 +596,13 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   float vD[kJ];
   issue_rows(pr, rD, 0, ltD, vD);
   uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
+  BM25_STAMP(7);
 
-  while (cD.rit < ngi) {
-    // (0) claim item n+4, (1) terms of item n+3, (2) bounds of item n+2
-    const Cursor cA = at(claim_read(pending));
-    pending = claim();
+  for (int32_t n = 0; n < count; ++n) {
+    // (1) terms of item n+3, (2) bounds of item n+2
     const int32_t tmA = terms_of(cA);
     const Desc dB = load_desc(a, tmB, tile_of<PH>(cB.ti, P));
+    BM25_STAMP(0);
     // (3) item n's second row block (issued before item n+1's rows so that
     //     its wait does not cover them), then item n+1's first rows
     const uint32_t nrD = rD.nrows;
@@ -630,6 +614,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     float vC[kJ];
     issue_rows(pr, rC, 0, ltC, vC);
     const uint64_t thC = PH == kRest ? theta[cC.qi] : 0ull;
+    BM25_STAMP(1);
     // (4) item n: adds in row order, then selection
     const int64_t tile = tile_of<PH>(cD.ti, P);
     add_rows(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ), mode);
@@ -645,8 +630,10 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
         add_rows(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ), mode);
       }
     }
+    BM25_STAMP(2);
     float fv[D / 64];
     take_entries<S>(acc, fv);
+    BM25_STAMP(3);
     if (mode & 4) {  // ablation: no selection
       if (fv[0] == 12345.f) cand[0] = 0;
     } else if (PH == kRest) {
@@ -654,10 +641,12 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     } else {
       select_top<S>(fv, tile, a.n_docs, kTileM, cand + ((int64_t)cD.qi * nt + cD.ti) * kTileM);
     }
+    BM25_STAMP(4);
     // rotate the pipeline
     cD = cC;
     cC = cB;
     cB = cA;
+    cA = next(cA, n + 3);
     tmD = tmC;
     tmC = tmB;
     tmB = tmA;
@@ -669,7 +658,15 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
       ltD[j] = ltC[j];
       vD[j] = vC[j];
     }
+    BM25_STAMP(5);
   }
+  if (stamps && lane_id() == 0) {
+    uint64_t* o = stamps + ((int64_t)blockIdx.x * kWaves + wave) * 8;
+    seg[6] = (uint64_t)count;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = seg[k];
+  }
+#undef BM25_STAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -1082,11 +1079,28 @@ static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const S
   if (use_pipe(ix, T)) {
     static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH>);
     static const int mode = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
-    int32_t* wctr = ws.wctr + 8 * (sg.qmap ? 2 : (PH == kRest ? 1 : 0));
-    hipMemsetAsync(wctr, 0, 8 * sizeof(int32_t), st);
+    uint64_t* stamps = nullptr;
+    if ((mode & 32) && PH == kRest) {  // diagnostic: per-segment cycles of the loop
+      static uint64_t* buf = nullptr;
+      if (!buf) hipMalloc(&buf, sizeof(uint64_t) * 8 * grid * kWaves);
+      hipMemsetAsync(buf, 0, sizeof(uint64_t) * 8 * grid * kWaves, st);
+      stamps = buf;
+    }
     hipLaunchKernelGGL((score_pipe_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0,
                        st, args_of(ix), q, (int32_t)T, sg, ws.theta, ws.cand, ws.list,
-                       ws.list_cnt, ws.list_cap, wctr, mode);
+                       ws.list_cnt, ws.list_cap, mode, stamps);
+    if (stamps) {
+      std::vector<uint64_t> h(8 * grid * kWaves);
+      hipStreamSynchronize(st);
+      hipMemcpy(h.data(), stamps, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost);
+      double tot[8] = {0};
+      for (size_t i = 0; i < h.size(); ++i) tot[i % 8] += (double)h[i];
+      double loop = 0;
+      for (int k = 0; k < 6; ++k) loop += tot[k];
+      fprintf(stderr, "stamps: items %.0f, per item:", tot[6]);
+      for (int k = 0; k < 6; ++k) fprintf(stderr, " s%d=%.0f", k, tot[k] / tot[6]);
+      fprintf(stderr, " | loop %.0f prologue %.0f (s_memtime ticks per wave)\n", loop / tot[6], tot[7] / (grid * kWaves));
+    }
     return;
   }
   static const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
