@@ -333,11 +333,133 @@ __device__ __forceinline__ void emit_above(const float (&fv)[(1 << S) / 64], int
   }
 }
 
+// ---------------------------------------------------------------------------
+// Selection straight from the LDS accumulators, 8 entries (2 float4) per lane
+// at a time, so no item keeps all 2^S/64 entries in registers.
+// ---------------------------------------------------------------------------
+// Key of entry e of this lane (0 past n_docs); `lim` = n_docs - tile base.
+__device__ __forceinline__ uint32_t entry_key(float f, int e, uint32_t lane, int lim) {
+  return (int)entry_doc(e, lane) < lim ? score_key(f) : 0u;
+}
+
+// This lane's best key over its entries (first of equal keys = smallest doc).
+template <int S>
+__device__ __forceinline__ void lane_best(const float* acc, int lim, uint32_t& bk, uint32_t& bd) {
+  const float4* a4 = reinterpret_cast<const float4*>(acc);
+  const uint32_t lane = lane_id();
+  bk = 0;
+  bd = 0;
+#pragma unroll 2
+  for (int j = 0; j < (1 << S) / 256; ++j) {
+    const float4 f = a4[j * 64 + lane];
+    const float fe[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t k = entry_key(fe[c], 4 * j + c, lane, lim);
+      if (k > bk) {
+        bk = k;
+        bd = entry_doc(4 * j + c, lane);
+      }
+    }
+  }
+}
+
+// SAMPLE / ALL tiles: the m best keys of the tile, best first, into out[0..m),
+// then the accumulators are cleared.  A round takes the wave's best key, then
+// the smallest doc among the lanes holding it; the winner marks that entry
+// taken (score bits 0xFFFFFFFF: key 0) and rescans its entries.
+template <int S>
+__device__ __forceinline__ void select_top_lds(float* acc, int64_t tile, int64_t n_docs, int m,
+                                               uint64_t* __restrict__ out) {
+  const uint32_t lane = lane_id();
+  const int64_t base = tile << S;
+  const int lim = (int)min<int64_t>(1 << S, n_docs - base);
+  uint32_t bk, bd;
+  lane_best<S>(acc, lim, bk, bd);
+  for (int r = 0; r < m; ++r) {
+    const uint32_t wm = wave_max_u32(bk);
+    if (wm == 0) {  // no valid entry left (tile smaller than m)
+      if (lane == 0) out[r] = 0;
+      continue;
+    }
+    const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk == wm ? 0xFFFFFFFFu - bd : 0u);
+    if (lane == ((doc >> 2) & 63u)) {
+      out[r] = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc));
+      acc[doc] = __uint_as_float(0xFFFFFFFFu);
+      lane_best<S>(acc, lim, bk, bd);
+    }
+  }
+  zero_acc<S>(acc);
+}
+
+// REST tiles: every key > theta is appended to the query's list (one atomic
+// per wave and chunk that has any), and the accumulators are cleared.  A list
+// that overflows its capacity C only counts: the merge sends that query to the
+// exact fallback stage.  The test runs on the fp32 sums (one compare per
+// entry, after a max early-out); only an entry equal to theta's score compares
+// doc ids.  Accumulators are never -0.0 (a sum that starts at +0.0 cannot
+// produce it); docs past n_docs are masked.
+template <int S>
+__device__ __forceinline__ void emit_rest(float* acc, int64_t tile, int64_t n_docs, uint64_t theta,
+                                          uint64_t* __restrict__ list, int32_t* __restrict__ cnt,
+                                          int32_t C) {
+  constexpr int D = 1 << S;
+  float4* a4 = reinterpret_cast<float4*>(acc);
+  const uint32_t lane = lane_id();
+  const float th = key_score((uint32_t)(theta >> 32));
+  const int64_t base = tile << S;
+  // tile-local bounds, clamped to [-1, D]: docs >= lim are past n_docs, ties
+  // pass for docs < tie
+  const int lim = (int)max<int64_t>(-1, min<int64_t>(D, n_docs - base));
+  const int tie = (int)max<int64_t>(
+      -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base));
+#pragma unroll 1
+  for (int j0 = 0; j0 < D / 256; j0 += 2) {  // not unrolled: 8 entries live at a time
+    const float4 f0 = a4[j0 * 64 + lane], f1 = a4[(j0 + 1) * 64 + lane];
+    a4[j0 * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    a4[(j0 + 1) * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float fe[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+    const float mx = fmaxf(fmaxf(fmaxf(fe[0], fe[1]), fmaxf(fe[2], fe[3])),
+                           fmaxf(fmaxf(fe[4], fe[5]), fmaxf(fe[6], fe[7])));
+    int c = 0;
+    if (!(mx < th && lim == D)) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int d = (int)entry_doc(4 * j0 + e, lane);
+        c += (d < lim) & ((fe[e] > th) | ((fe[e] == th) & (d < tie)));
+      }
+    }
+    if (__ballot(c > 0) == 0) continue;  // common: nothing of this chunk passes
+    const uint32_t incl = wave_incl_scan((uint32_t)c);
+    int pos = 0;
+    if (lane == 63) pos = atomicAdd(cnt, (int)incl);
+    pos = __shfl(pos, 63, 64) + (int)incl - c;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int d = (int)entry_doc(4 * j0 + e, lane);
+      const bool pass = (d < lim) & ((fe[e] > th) | ((fe[e] == th) & (d < tie)));
+      if (pass) {
+        if (pos < C)
+          list[pos] = ((uint64_t)score_key(fe[e]) << 32) |
+                      (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + d));
+        ++pos;
+      }
+    }
+  }
+}
+
 template <int PH>
 __device__ __forceinline__ int64_t tile_of(int64_t ti, int P) {
   if (PH == kAll) return ti;
   if (PH == kSample) return ti * P;
   return (ti / (P - 1)) * P + (ti % (P - 1)) + 1;
+}
+template <int PH>
+__device__ __forceinline__ int32_t tile_of32(uint32_t ti, uint32_t P) {
+  if (PH == kAll) return (int32_t)ti;
+  if (PH == kSample) return (int32_t)(ti * P);
+  const uint32_t g = ti / (P - 1u);
+  return (int32_t)(g * P + (ti - g * (P - 1u)) + 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -382,6 +504,7 @@ __device__ __forceinline__ uint32_t scan16(uint32_t x) {
 struct Rows {
   int64_t base;    // posting index of the row's first posting (0 past the end)
   uint32_t cnt;    // postings in the row (0: past the item's rows)
+  uint32_t term;   // the row's query term (T past the end)
   uint32_t nrows;  // rows of the item (uniform)
 };
 
@@ -411,6 +534,7 @@ __device__ __forceinline__ Rows make_rows(const Desc& d, int T, uint32_t j0) {
   const bool in = j < r.nrows;
   r.base = in ? (int64_t)(((uint64_t)bhi << 32) | blo) + 64 * (int64_t)k : 0;
   r.cnt = in ? min(64u, l - 64u * k) : 0u;
+  r.term = in ? (uint32_t)pos : (uint32_t)T;
   return r;
 }
 
@@ -446,31 +570,47 @@ __device__ __forceinline__ void issue_rows(const PostingRsrc& pr, const Rows& R,
   }
 }
 
-// The first n (uniform) of the loaded rows, in order: ds_read, add,
-// ds_write per row.  A row's docs are distinct (one term), and the LDS
-// executes a wave's instructions in order, so row j+1's read sees row j's
-// write.  (An LDS float atomic does the same add at ~2.5x the cost on
-// gfx950: 23.8 vs 10.9 ms for the config-3 score pass, BM25_ABLATE=8.)
+// The first n (uniform) of the loaded rows, in order.  Per row: ds_read,
+// add, ds_write (an LDS float atomic does the same add at ~2.5x the cost on
+// gfx950: 23.8 vs 10.9 ms for the config-3 score pass).  A run of rows of one
+// term holds distinct docs, so its reads are issued together and its writes
+// after one wait; before the first read of the next term every pending write
+// is issued, and the LDS executes a wave's instructions in order, so each
+// doc's adds stay in query-term order.
+template <int DIAG>
 __device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0,
                                          const uint32_t (&ld)[kJ], const float (&v)[kJ],
-                                         uint32_t n, int mode) {
+                                         uint32_t n) {
   const uint32_t lane = lane_id();
-  if (mode & 1) {  // ablation: consume the loads, no adds
+  if (DIAG & 1) {  // ablation: consume the loads, no adds
 #pragma unroll
     for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
     return;
   }
+  float x[kJ];
+  uint32_t pend = 0, tprev = ~0u;
+  auto flush = [&](int upto) {
+#pragma unroll
+    for (int i = 0; i < kJ; ++i)
+      if (i < upto && (pend >> i) & 1u)
+        if (lane < lane_u32(R.cnt, j0 + i)) acc[ld[i]] = x[i] + v[i];
+    pend = 0;
+  };
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
-    if ((uint32_t)j < n && lane < lane_u32(R.cnt, j0 + j)) {
-      if (mode & 8) lds_add(acc + ld[j], v[j]);  // ablation: LDS float atomics
-      else acc[ld[j]] = acc[ld[j]] + v[j];
+    if ((uint32_t)j < n) {
+      const uint32_t tj = lane_u32(R.term, j0 + j);
+      if (tj != tprev) flush(j);
+      tprev = tj;
+      if (lane < lane_u32(R.cnt, j0 + j)) x[j] = acc[ld[j]];
+      pend |= 1u << j;
     }
   }
+  flush(kJ);
 }
 
-struct Cursor {  // item it0 + n*stride as (ti, qi)
-  int32_t ti, qi;
+struct Cursor {  // item it0 + n*stride as (ti, qi) and its tile
+  int32_t ti, qi, tile;
 };
 
 // ---------------------------------------------------------------------------
@@ -527,19 +667,20 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
 // and then (4) adding item n's rows (a heavy item's further rows are loaded in
 // place) and selecting / emitting its candidates.
 // ---------------------------------------------------------------------------
-template <int S, int PH>
+template <int S, int PH, bool QMAP, int DIAG>
 __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
-    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, Stage sg,
+    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t nq_host,
+    const int32_t* __restrict__ nq_dev, const int32_t* __restrict__ qmap,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
-    int32_t* __restrict__ list_cnt, int32_t C, int mode, uint64_t* __restrict__ stamps) {
+    int32_t* __restrict__ list_cnt, int32_t C, uint64_t* __restrict__ stamps) {
   constexpr int D = 1 << S;
   __shared__ __attribute__((aligned(16))) float acc_all[kWaves * D];
   const int wave = uniform((int)(threadIdx.x >> 6));
   float* acc = acc_all + wave * D;
-  // diagnostic build only (BM25_ABLATE & 32): cycles per loop segment
+  // diagnostic build only (DIAG & 32): cycles per loop segment
   uint64_t seg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = 0;
 #define BM25_STAMP(k)                                                           \
-  if (stamps) {                                                                 \
+  if (DIAG & 32) {                                                              \
     __builtin_amdgcn_sched_barrier(0);                                          \
     uint64_t t_;                                                                \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
@@ -548,8 +689,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     t_last = t_;                                                                \
   }
   BM25_STAMP(7);
-  const int32_t nq = sg.nq_dev ? *sg.nq_dev : sg.nq_host;
-  const int P = sg.P;
+  const int32_t nq = QMAP ? *nq_dev : nq_host;
   const int32_t nS = (int32_t)((a.ntiles + P - 1) / P);
   const int32_t nt = PH == kAll ? (int32_t)a.ntiles : (PH == kSample ? nS : (int32_t)a.ntiles - nS);
   const int64_t nitems = (int64_t)nt * nq;
@@ -575,11 +715,12 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
         c.qi -= nq;
         ++c.ti;
       }
+      c.tile = tile_of32<PH>((uint32_t)c.ti, (uint32_t)P);
     }
     return c;
   };
   auto terms_of = [&](const Cursor& c) -> int32_t {
-    const int32_t q = sg.qmap ? sg.qmap[c.qi] : c.qi;
+    const int32_t q = QMAP ? qmap[c.qi] : c.qi;
     return queries[(int64_t)q * T + tl];
   };
 
@@ -587,11 +728,12 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   Cursor cD;
   cD.ti = (int32_t)(it0 / nq);
   cD.qi = (int32_t)(it0 - (int64_t)cD.ti * nq);
+  cD.tile = tile_of32<PH>((uint32_t)cD.ti, (uint32_t)P);
   Cursor cC = next(cD, 0), cB = next(cC, 1), cA = next(cB, 2);
   // prologue: item 0's first rows, item 1's bounds, item 2's terms
   int32_t tmD = terms_of(cD), tmC = terms_of(cC), tmB = terms_of(cB);
-  Desc dC = load_desc(a, tmC, tile_of<PH>(cC.ti, P));
-  Rows rD = make_rows(load_desc(a, tmD, tile_of<PH>(cD.ti, P)), T, 0);
+  Desc dC = load_desc(a, tmC, cC.tile);
+  Rows rD = make_rows(load_desc(a, tmD, cD.tile), T, 0);
   uint32_t ltD[kJ];
   float vD[kJ];
   issue_rows(pr, rD, 0, ltD, vD);
@@ -599,26 +741,25 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   BM25_STAMP(7);
 
   for (int32_t n = 0; n < count; ++n) {
-    // (1) terms of item n+3, (2) bounds of item n+2
-    const int32_t tmA = terms_of(cA);
-    const Desc dB = load_desc(a, tmB, tile_of<PH>(cB.ti, P));
-    BM25_STAMP(0);
-    // (3) item n's second row block (issued before item n+1's rows so that
-    //     its wait does not cover them), then item n+1's first rows
+    // (1) item n's second row block, (2) terms of item n+3, (3) bounds of
+    // item n+2, (4) item n+1's first rows: all issued before item n's adds
     const uint32_t nrD = rD.nrows;
     uint32_t ltX[kJ];
     float vX[kJ];
     if (nrD > kJ) issue_rows(pr, rD, kJ, ltX, vX);
+    const int32_t tmA = terms_of(cA);
+    const Desc dB = load_desc(a, tmB, cB.tile);
+    BM25_STAMP(0);
     const Rows rC = make_rows(dC, T, 0);
     uint32_t ltC[kJ];
     float vC[kJ];
     issue_rows(pr, rC, 0, ltC, vC);
     const uint64_t thC = PH == kRest ? theta[cC.qi] : 0ull;
     BM25_STAMP(1);
-    // (4) item n: adds in row order, then selection
-    const int64_t tile = tile_of<PH>(cD.ti, P);
-    add_rows(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ), mode);
-    if (nrD > kJ) add_rows(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ), mode);
+    // (5) item n: adds in row order, then selection
+    const int64_t tile = cD.tile;
+    add_rows<DIAG>(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ));
+    if (nrD > kJ) add_rows<DIAG>(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ));
     if (nrD > 2 * kJ) {  // heavy item: the remaining rows, block by block
       const Desc dD = load_desc(a, tmD, tile);
       Rows t = rD;
@@ -627,19 +768,17 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
         uint32_t ltY[kJ];
         float vY[kJ];
         issue_rows(pr, t, (int)(j & 63), ltY, vY);
-        add_rows(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ), mode);
+        add_rows<DIAG>(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ));
       }
     }
     BM25_STAMP(2);
-    float fv[D / 64];
-    take_entries<S>(acc, fv);
     BM25_STAMP(3);
-    if (mode & 4) {  // ablation: no selection
-      if (fv[0] == 12345.f) cand[0] = 0;
+    if (DIAG & 4) {  // ablation: no selection
+      zero_acc<S>(acc);
     } else if (PH == kRest) {
-      emit_above<S>(fv, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
+      emit_rest<S>(acc, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
     } else {
-      select_top<S>(fv, tile, a.n_docs, kTileM, cand + ((int64_t)cD.qi * nt + cD.ti) * kTileM);
+      select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + ((int64_t)cD.qi * nt + cD.ti) * kTileM);
     }
     BM25_STAMP(4);
     // rotate the pipeline
@@ -660,7 +799,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     }
     BM25_STAMP(5);
   }
-  if (stamps && lane_id() == 0) {
+  if ((DIAG & 32) && lane_id() == 0) {
     uint64_t* o = stamps + ((int64_t)blockIdx.x * kWaves + wave) * 8;
     seg[6] = (uint64_t)count;
 #pragma unroll
@@ -1073,34 +1212,55 @@ static bool use_pipe(const DevIndex& ix, int64_t T) {
   return !off && T >= 1 && T <= kGroup && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
 }
 
+// Diagnostic builds (BM25_ABLATE, dev only): 1 = no adds, 4 = no selection,
+// 5 = neither, 32 = s_memtime segment stamps of the REST kernel, printed to
+// stderr per launch.
+template <int S, int PH, bool QMAP, int DIAG>
+static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
+                        const Workspace& ws, hipStream_t st) {
+  static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH, QMAP, DIAG>);
+  uint64_t* stamps = nullptr;
+  if (DIAG & 32) {
+    static uint64_t* buf = nullptr;
+    if (!buf) hipMalloc(&buf, sizeof(uint64_t) * 8 * grid * kWaves);
+    hipMemsetAsync(buf, 0, sizeof(uint64_t) * 8 * grid * kWaves, st);
+    stamps = buf;
+  }
+  hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG>), dim3((unsigned)grid),
+                     dim3(64 * kWaves), 0, st, args_of(ix), q, (int32_t)T, sg.P, sg.nq_host,
+                     sg.nq_dev, sg.qmap, ws.theta, ws.cand, ws.list, ws.list_cnt, ws.list_cap,
+                     stamps);
+  if ((DIAG & 32) && PH == kRest) {
+    std::vector<uint64_t> h(8 * grid * kWaves);
+    hipStreamSynchronize(st);
+    hipMemcpy(h.data(), stamps, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost);
+    double tot[8] = {0};
+    for (size_t i = 0; i < h.size(); ++i) tot[i % 8] += (double)h[i];
+    double loop = 0;
+    for (int k = 0; k < 6; ++k) loop += tot[k];
+    fprintf(stderr, "stamps: items %.0f, per item:", tot[6]);
+    for (int k = 0; k < 6; ++k) fprintf(stderr, " s%d=%.0f", k, tot[k] / tot[6]);
+    fprintf(stderr, " | loop %.0f (s_memtime ticks per wave)\n", loop / tot[6]);
+  }
+}
+
 template <int S, int PH>
 static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
                         const Workspace& ws, hipStream_t st) {
   if (use_pipe(ix, T)) {
-    static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH>);
-    static const int mode = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
-    uint64_t* stamps = nullptr;
-    if ((mode & 32) && PH == kRest) {  // diagnostic: per-segment cycles of the loop
-      static uint64_t* buf = nullptr;
-      if (!buf) hipMalloc(&buf, sizeof(uint64_t) * 8 * grid * kWaves);
-      hipMemsetAsync(buf, 0, sizeof(uint64_t) * 8 * grid * kWaves, st);
-      stamps = buf;
-    }
-    hipLaunchKernelGGL((score_pipe_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0,
-                       st, args_of(ix), q, (int32_t)T, sg, ws.theta, ws.cand, ws.list,
-                       ws.list_cnt, ws.list_cap, mode, stamps);
-    if (stamps) {
-      std::vector<uint64_t> h(8 * grid * kWaves);
-      hipStreamSynchronize(st);
-      hipMemcpy(h.data(), stamps, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost);
-      double tot[8] = {0};
-      for (size_t i = 0; i < h.size(); ++i) tot[i % 8] += (double)h[i];
-      double loop = 0;
-      for (int k = 0; k < 6; ++k) loop += tot[k];
-      fprintf(stderr, "stamps: items %.0f, per item:", tot[6]);
-      for (int k = 0; k < 6; ++k) fprintf(stderr, " s%d=%.0f", k, tot[k] / tot[6]);
-      fprintf(stderr, " | loop %.0f prologue %.0f (s_memtime ticks per wave)\n", loop / tot[6], tot[7] / (grid * kWaves));
-    }
+    static const int diag = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
+    if (sg.qmap)
+      launch_pipe<S, PH, true, 0>(ix, q, T, sg, ws, st);
+    else if (diag == 0)
+      launch_pipe<S, PH, false, 0>(ix, q, T, sg, ws, st);
+    else if (diag == 1)
+      launch_pipe<S, PH, false, 1>(ix, q, T, sg, ws, st);
+    else if (diag == 4)
+      launch_pipe<S, PH, false, 4>(ix, q, T, sg, ws, st);
+    else if (diag == 5)
+      launch_pipe<S, PH, false, 5>(ix, q, T, sg, ws, st);
+    else
+      launch_pipe<S, PH, false, 32>(ix, q, T, sg, ws, st);
     return;
   }
   static const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
