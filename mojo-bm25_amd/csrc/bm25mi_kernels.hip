@@ -609,6 +609,59 @@ __device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0,
   flush(kJ);
 }
 
+// REST emission from the item's own postings (items of at most 2 kJ rows,
+// whose slots are still in registers): each touched doc's final sum is read
+// once — the first read of a doc clears it, so a doc seen again under a later
+// term reads 0 — and passes iff its key beats theta.  Exact when theta's
+// score is > 0: untouched docs (sum 0) and cleared re-reads can never pass,
+// and every touched doc is read after its last add.  The same reads return
+// the accumulator to all zeros for the next item.
+__device__ __forceinline__ void emit_sparse(float* acc, const Rows& R, const uint32_t (&l0)[kJ],
+                                            const uint32_t (&l1)[kJ], uint32_t nr, int64_t tile,
+                                            int S, uint64_t theta, uint64_t* __restrict__ list,
+                                            int32_t* __restrict__ cnt, int32_t C) {
+  const uint32_t lane = lane_id();
+  float x[2 * kJ];
+#pragma unroll
+  for (int j = 0; j < 2 * kJ; ++j) {
+    x[j] = 0.f;
+    if ((uint32_t)j < nr) {
+      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
+      if (lane < lane_u32(R.cnt, j)) {
+        x[j] = acc[l];
+        acc[l] = 0.f;
+      }
+    }
+  }
+  const float th = key_score((uint32_t)(theta >> 32));
+  const int64_t base = tile << S;
+  // ties pass for tile-local docs < tie (clamped to [-1, 2^S])
+  const int tie = (int)max<int64_t>(
+      -1, min<int64_t>(1 << S, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base));
+  uint32_t pm = 0;
+#pragma unroll
+  for (int j = 0; j < 2 * kJ; ++j) {
+    const int l = (int)(j < kJ ? l0[j] : l1[j - kJ]);
+    pm |= (uint32_t)((x[j] > th) | ((x[j] == th) & (l < tie))) << j;
+  }
+  if (__ballot(pm != 0) == 0) return;  // common: nothing of this item passes
+  const int c = __popc(pm);
+  const uint32_t incl = wave_incl_scan((uint32_t)c);
+  int pos = 0;
+  if (lane == 63) pos = atomicAdd(cnt, (int)incl);
+  pos = __shfl(pos, 63, 64) + (int)incl - c;
+#pragma unroll
+  for (int j = 0; j < 2 * kJ; ++j) {
+    if ((pm >> j) & 1u) {
+      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
+      if (pos < C)
+        list[pos] = ((uint64_t)score_key(x[j]) << 32) |
+                    (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + l));
+      ++pos;
+    }
+  }
+}
+
 struct Cursor {  // item it0 + n*stride as (ti, qi) and its tile
   int32_t ti, qi, tile;
 };
@@ -760,21 +813,38 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     const int64_t tile = cD.tile;
     add_rows<DIAG>(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ));
     if (nrD > kJ) add_rows<DIAG>(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ));
-    if (nrD > 2 * kJ) {  // heavy item: the remaining rows, block by block
+    if (nrD > 2 * kJ) {  // heavy item: the remaining rows, block j + kJ issued before block j's adds
       const Desc dD = load_desc(a, tmD, tile);
       Rows t = rD;
+      if ((2 * kJ & 63) == 0) t = make_rows(dD, T, 2 * kJ);
+      uint32_t ltY[kJ];
+      float vY[kJ];
+      issue_rows(pr, t, (2 * kJ) & 63, ltY, vY);
       for (uint32_t j = 2 * kJ; j < nrD; j += kJ) {
-        if ((j & 63) == 0) t = make_rows(dD, T, j);
-        uint32_t ltY[kJ];
-        float vY[kJ];
-        issue_rows(pr, t, (int)(j & 63), ltY, vY);
+        const uint32_t jn = j + kJ;
+        Rows tn = t;
+        uint32_t ltZ[kJ];
+        float vZ[kJ];
+        if (jn < nrD) {
+          if ((jn & 63) == 0) tn = make_rows(dD, T, jn);
+          issue_rows(pr, tn, (int)(jn & 63), ltZ, vZ);
+        }
         add_rows<DIAG>(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ));
+        t = tn;
+#pragma unroll
+        for (int i = 0; i < kJ; ++i) {
+          ltY[i] = ltZ[i];
+          vY[i] = vZ[i];
+        }
       }
     }
     BM25_STAMP(2);
     BM25_STAMP(3);
     if (DIAG & 4) {  // ablation: no selection
       zero_acc<S>(acc);
+    } else if (PH == kRest && nrD <= 2 * kJ && (uint32_t)(thD >> 32) > score_key(0.f)) {
+      emit_sparse(acc, rD, ltD, ltX, nrD, tile, S, thD, list + (int64_t)cD.qi * C,
+                  list_cnt + cD.qi, C);
     } else if (PH == kRest) {
       emit_rest<S>(acc, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
     } else {

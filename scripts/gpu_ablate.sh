@@ -4,6 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 for var in ${VARIANTS:-BM25_TILE_SHIFT=13}; do
   envs=$(echo "$var" | tr ',' ' ')
-  env $envs timeout -k 10 180 python scripts/ablate.py ${CFG:-c3} | sed "s/}/, \"variant\": \"$var\"}/" >> gpurun_out/ablate.jsonl 2>> gpurun_out/ablate.err || exit $?
+  echo "== $var" >> gpurun_out/ablate.err
+  env $envs timeout -k 10 180 python scripts/ablate.py ${CFG:-c3} 2>> gpurun_out/ablate.err | sed "s/}/, \"variant\": \"$var\"}/" >> gpurun_out/ablate.jsonl || exit $?
 done
 echo ablate done
