@@ -88,6 +88,7 @@ void free_ws(Workspace& ws) {
   hipFree(ws.nflag);
   hipFree(ws.queue);
   hipFree(ws.counters);
+  hipFree(ws.wctr);
   ws = Workspace{};
 }
 
@@ -121,6 +122,7 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
   HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
   HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * 4), "hipMemset(counters)");
+  HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrInts), "hipMalloc(wctr)");
   ws.list_cap = C;
   ws.cap_q = q;
   ws.cap_k = kk;

@@ -47,6 +47,13 @@ constexpr int64_t kPostingPad = 64;
 // Default tile: 2^11 = 2048 docs, one wavefront's LDS accumulator (8 KB).
 constexpr int kDefaultTileShift = 11;
 
+// Item claims of the pipelined score kernel (bm25mi_kernels.hip): items per
+// claim, counters per XCD, int32 stride between counters (256 B).
+constexpr int kClaimCH = 8;
+constexpr int kClaimM = 4;
+constexpr int kCtrStride = 64;
+constexpr int kWctrInts = 8 * kClaimM * kCtrStride;
+
 struct DevIndex {
   int device = 0;
   int64_t n_docs = 0, n_terms = 0, nnz = 0, doc_offset = 0;
@@ -72,6 +79,7 @@ struct Workspace {
   int32_t* queue = nullptr;      // [Q*maxflag] items = qi*maxflag + i
   int32_t* counters = nullptr;   // [0]/[1] rescore queue length / pop cursor,
                                  // [2] fallback queries, [3] tiles re-scored this search
+  int32_t* wctr = nullptr;       // [kWctrInts] item-claim counters, zeroed before each score launch
 };
 
 // Flag slots per query: a flagged tile holds kTileM keys of the top-(k-1), so

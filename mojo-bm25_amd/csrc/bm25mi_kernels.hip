@@ -662,8 +662,18 @@ __device__ __forceinline__ void emit_sparse(float* acc, const Rows& R, const uin
   }
 }
 
-struct Cursor {  // item it0 + n*stride as (ti, qi) and its tile
-  int32_t ti, qi, tile;
+// Item distribution of the pipelined kernel.  An XCD's items (one contiguous
+// range of the tile-major item order per XCD) are handed out kClaimCH at a
+// time by kClaimM counters per XCD (counter c serves chunks c, c + kClaimM,
+// ...; each on a 256-B line of its own), so at any moment the XCD's waves work
+// on a window of about (waves x kClaimCH) consecutive items: a few tiles, whose
+// posting segments stay in the XCD's L2 across the queries.  A static stride
+// lets waves drift apart (items differ in cost) until the window spans far more
+// tiles than L2 holds.
+// (kClaimCH, kClaimM, kCtrStride: bm25mi_internal.h)
+
+struct Cursor {  // XCD-relative item rit = (ti, qi) and its tile; end = its chunk's end
+  int32_t rit, end, ti, qi, tile;
 };
 
 // ---------------------------------------------------------------------------
@@ -725,7 +735,8 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t nq_host,
     const int32_t* __restrict__ nq_dev, const int32_t* __restrict__ qmap,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
-    int32_t* __restrict__ list_cnt, int32_t C, uint64_t* __restrict__ stamps) {
+    int32_t* __restrict__ list_cnt, int32_t C, int32_t* __restrict__ wctr,
+    uint64_t* __restrict__ stamps) {
   constexpr int D = 1 << S;
   __shared__ __attribute__((aligned(16))) float acc_all[kWaves * D];
   const int wave = uniform((int)(threadIdx.x >> 6));
@@ -747,42 +758,65 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   const int32_t nt = PH == kAll ? (int32_t)a.ntiles : (PH == kSample ? nS : (int32_t)a.ntiles - nS);
   const int64_t nitems = (int64_t)nt * nq;
   const int64_t per = (nitems + 7) >> 3;
-  const int64_t grp = blockIdx.x & 7;
-  const int64_t lo = grp * per;
-  const int64_t hi = min(nitems, lo + per);
-  const int32_t stride = (int32_t)(gridDim.x >> 3) * kWaves;
-  const int64_t it0 = lo + (int64_t)(blockIdx.x >> 3) * kWaves + wave;
-  if (it0 >= hi) return;  // wave-uniform; no barriers in this kernel
-  const int32_t count = (int32_t)((hi - it0 + stride - 1) / stride);
-  const int32_t sdiv = stride / nq, smod = stride - sdiv * nq;
+  const int grp = (int)(blockIdx.x & 7);
+  const uint32_t lo = (uint32_t)(grp * per);
+  const int32_t ngi = (int32_t)max<int64_t>(0, min<int64_t>(nitems, lo + per) - lo);
+  if (ngi == 0) return;  // wave-uniform; no barriers in this kernel
+  const int32_t cm = (int32_t)((blockIdx.x >> 3) * kWaves + wave) % kClaimM;
+  int32_t* ctr = wctr + (grp * kClaimM + cm) * kCtrStride;
   const int tl = min(lane_id(), T - 1);
   const PostingRsrc pr = posting_rsrc(a);
 
-  // cursor of item n+1 from item n's (stays on the last item past the end,
-  // so every stage keeps loading valid addresses)
-  auto next = [&](Cursor c, int32_t n) -> Cursor {
-    if (n + 1 < count) {
-      c.ti += sdiv;
-      c.qi += smod;
-      if (c.qi >= nq) {
-        c.qi -= nq;
+  // Claims: lane 0 holds the ordinal of the wave's next chunk on its counter,
+  // claimed one chunk ahead of use.
+  auto claim = [&]() -> int32_t {
+    int32_t v = 0;
+    if (lane_id() == 0) v = atomicAdd(ctr, 1);
+    return v;
+  };
+  int32_t pending = claim();
+  // cursor of the next item after c: the next one of c's chunk, else the
+  // first of the pending chunk; past the end it stays on c's item with
+  // rit = ngi, so every stage keeps loading valid addresses
+  auto next = [&](Cursor c) -> Cursor {
+    if (c.rit >= ngi) return c;
+    if (c.rit + 1 < c.end) {
+      ++c.rit;
+      if (++c.qi == nq) {
+        c.qi = 0;
         ++c.ti;
       }
       c.tile = tile_of32<PH>((uint32_t)c.ti, (uint32_t)P);
+      return c;
     }
-    return c;
+    const int64_t b = ((int64_t)uniform(pending) * kClaimM + cm) * kClaimCH;
+    if (b >= ngi) {
+      c.rit = c.end = ngi;
+      return c;
+    }
+    pending = claim();
+    Cursor n;
+    n.rit = (int32_t)b;
+    n.end = (int32_t)min<int64_t>(ngi, b + kClaimCH);
+    const uint32_t it = lo + (uint32_t)b;
+    n.ti = (int32_t)(it / (uint32_t)nq);
+    n.qi = (int32_t)(it - (uint32_t)n.ti * (uint32_t)nq);
+    n.tile = tile_of32<PH>((uint32_t)n.ti, (uint32_t)P);
+    return n;
   };
   auto terms_of = [&](const Cursor& c) -> int32_t {
     const int32_t q = QMAP ? qmap[c.qi] : c.qi;
     return queries[(int64_t)q * T + tl];
   };
 
+  Cursor c0;  // a chunk "before" the first one: next() takes the pending claim
+  c0.rit = -1;
+  c0.end = 0;
+  c0.ti = c0.qi = c0.tile = 0;
+  Cursor cD = next(c0);
+  if (cD.rit >= ngi) return;
   zero_acc<S>(acc);
-  Cursor cD;
-  cD.ti = (int32_t)(it0 / nq);
-  cD.qi = (int32_t)(it0 - (int64_t)cD.ti * nq);
-  cD.tile = tile_of32<PH>((uint32_t)cD.ti, (uint32_t)P);
-  Cursor cC = next(cD, 0), cB = next(cC, 1), cA = next(cB, 2);
+  Cursor cC = next(cD), cB = next(cC), cA = next(cB);
   // prologue: item 0's first rows, item 1's bounds, item 2's terms
   int32_t tmD = terms_of(cD), tmC = terms_of(cC), tmB = terms_of(cB);
   Desc dC = load_desc(a, tmC, cC.tile);
@@ -791,9 +825,11 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   float vD[kJ];
   issue_rows(pr, rD, 0, ltD, vD);
   uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
+  int32_t nitem = 0;
   BM25_STAMP(7);
 
-  for (int32_t n = 0; n < count; ++n) {
+  while (cD.rit < ngi) {
+    ++nitem;
     // (1) item n's second row block, (2) terms of item n+3, (3) bounds of
     // item n+2, (4) item n+1's first rows: all issued before item n's adds
     const uint32_t nrD = rD.nrows;
@@ -855,7 +891,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     cD = cC;
     cC = cB;
     cB = cA;
-    cA = next(cA, n + 3);
+    cA = next(cA);
     tmD = tmC;
     tmC = tmB;
     tmB = tmA;
@@ -871,7 +907,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   }
   if ((DIAG & 32) && lane_id() == 0) {
     uint64_t* o = stamps + ((int64_t)blockIdx.x * kWaves + wave) * 8;
-    seg[6] = (uint64_t)count;
+    seg[6] = (uint64_t)nitem;
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = seg[k];
   }
@@ -1289,6 +1325,7 @@ template <int S, int PH, bool QMAP, int DIAG>
 static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
                         const Workspace& ws, hipStream_t st) {
   static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH, QMAP, DIAG>);
+  hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrInts, st);
   uint64_t* stamps = nullptr;
   if (DIAG & 32) {
     static uint64_t* buf = nullptr;
@@ -1299,7 +1336,7 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
   hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG>), dim3((unsigned)grid),
                      dim3(64 * kWaves), 0, st, args_of(ix), q, (int32_t)T, sg.P, sg.nq_host,
                      sg.nq_dev, sg.qmap, ws.theta, ws.cand, ws.list, ws.list_cnt, ws.list_cap,
-                     stamps);
+                     ws.wctr, stamps);
   if ((DIAG & 32) && PH == kRest) {
     std::vector<uint64_t> h(8 * grid * kWaves);
     hipStreamSynchronize(st);
@@ -1317,7 +1354,7 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
 template <int S, int PH>
 static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
                         const Workspace& ws, hipStream_t st) {
-  if (use_pipe(ix, T)) {
+  if (use_pipe(ix, T) && ix.ntiles * (int64_t)sg.nq_host < 0x7FFFFFFFll) {
     static const int diag = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
     if (sg.qmap)
       launch_pipe<S, PH, true, 0>(ix, q, T, sg, ws, st);
