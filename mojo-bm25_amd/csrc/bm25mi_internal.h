@@ -50,7 +50,7 @@ constexpr int kDefaultTileShift = 11;
 // Item claims of the pipelined score kernel (bm25mi_kernels.hip): items per
 // claim, counters per XCD, int32 stride between counters (256 B).
 constexpr int kClaimCH = 8;
-constexpr int kClaimM = 4;
+constexpr int kClaimM = 8;  // counters allocated per XCD (4 used by default)
 constexpr int kCtrStride = 64;
 constexpr int kWctrInts = 8 * kClaimM * kCtrStride;
 

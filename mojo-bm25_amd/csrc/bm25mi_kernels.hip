@@ -577,36 +577,50 @@ __device__ __forceinline__ void issue_rows(const PostingRsrc& pr, const Rows& R,
 // after one wait; before the first read of the next term every pending write
 // is issued, and the LDS executes a wave's instructions in order, so each
 // doc's adds stay in query-term order.
-template <int DIAG>
-__device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0,
-                                         const uint32_t (&ld)[kJ], const float (&v)[kJ],
-                                         uint32_t n) {
+//
+// Lanes past a row's postings are redirected to the lane's own trash slot
+// (acc[2^S + lane], always 0) with a zero score, so every LDS access runs
+// unmasked: no exec-mask branches, and the compiler keeps its lgkmcnt waits
+// counted.  The redirected slots are written back into ld for the sparse
+// emission.
+template <int S, int DIAG>
+__device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0, uint32_t (&ld)[kJ],
+                                         float (&v)[kJ], uint32_t n) {
   const uint32_t lane = lane_id();
+  const uint32_t trash = (1u << S) + lane;
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    if ((uint32_t)j < n) {
+      const bool m = lane < lane_u32(R.cnt, j0 + j);
+      ld[j] = m ? ld[j] : trash;
+      v[j] = m ? v[j] : 0.f;
+    }
+  }
   if (DIAG & 1) {  // ablation: consume the loads, no adds
 #pragma unroll
     for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
     return;
   }
   float x[kJ];
-  uint32_t pend = 0, tprev = ~0u;
-  auto flush = [&](int upto) {
-#pragma unroll
-    for (int i = 0; i < kJ; ++i)
-      if (i < upto && (pend >> i) & 1u)
-        if (lane < lane_u32(R.cnt, j0 + i)) acc[ld[i]] = x[i] + v[i];
-    pend = 0;
-  };
+  uint32_t tprev = ~0u;
+  int f = 0;  // rows [f, j) read, not yet written
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
     if ((uint32_t)j < n) {
       const uint32_t tj = lane_u32(R.term, j0 + j);
-      if (tj != tprev) flush(j);
+      if (tj != tprev) {  // a new term: the earlier rows' writes go first
+#pragma unroll
+        for (int i = 0; i < j; ++i)
+          if (i >= f) acc[ld[i]] = x[i] + v[i];
+        f = j;
+      }
       tprev = tj;
-      if (lane < lane_u32(R.cnt, j0 + j)) x[j] = acc[ld[j]];
-      pend |= 1u << j;
+      x[j] = acc[ld[j]];
     }
   }
-  flush(kJ);
+#pragma unroll
+  for (int i = 0; i < kJ; ++i)
+    if (i >= f && (uint32_t)i < n) acc[ld[i]] = x[i] + v[i];
 }
 
 // REST emission from the item's own postings (items of at most 2 kJ rows,
@@ -615,8 +629,9 @@ __device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0,
 // term reads 0 — and passes iff its key beats theta.  Exact when theta's
 // score is > 0: untouched docs (sum 0) and cleared re-reads can never pass,
 // and every touched doc is read after its last add.  The same reads return
-// the accumulator to all zeros for the next item.
-__device__ __forceinline__ void emit_sparse(float* acc, const Rows& R, const uint32_t (&l0)[kJ],
+// the accumulator to all zeros for the next item.  Slots are add_rows'
+// (lanes past a row's postings hold their trash slot, which reads 0).
+__device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ],
                                             const uint32_t (&l1)[kJ], uint32_t nr, int64_t tile,
                                             int S, uint64_t theta, uint64_t* __restrict__ list,
                                             int32_t* __restrict__ cnt, int32_t C) {
@@ -627,10 +642,8 @@ __device__ __forceinline__ void emit_sparse(float* acc, const Rows& R, const uin
     x[j] = 0.f;
     if ((uint32_t)j < nr) {
       const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
-      if (lane < lane_u32(R.cnt, j)) {
-        x[j] = acc[l];
-        acc[l] = 0.f;
-      }
+      x[j] = acc[l];
+      acc[l] = 0.f;
     }
   }
   const float th = key_score((uint32_t)(theta >> 32));
@@ -731,16 +744,17 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
 // place) and selecting / emitting its candidates.
 // ---------------------------------------------------------------------------
 template <int S, int PH, bool QMAP, int DIAG>
-__global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 4))) void score_pipe_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t nq_host,
     const int32_t* __restrict__ nq_dev, const int32_t* __restrict__ qmap,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
-    int32_t* __restrict__ list_cnt, int32_t C, int32_t* __restrict__ wctr,
-    uint64_t* __restrict__ stamps) {
+    int32_t* __restrict__ list_cnt, int32_t C, int32_t* __restrict__ wctr, int32_t claim_ch,
+    int32_t claim_m, uint64_t* __restrict__ stamps) {
   constexpr int D = 1 << S;
-  __shared__ __attribute__((aligned(16))) float acc_all[kWaves * D];
+  constexpr int DP = D + 64;  // accumulators + one trash slot per lane (add_rows)
+  __shared__ __attribute__((aligned(16))) float acc_all[kWaves * DP];
   const int wave = uniform((int)(threadIdx.x >> 6));
-  float* acc = acc_all + wave * D;
+  float* acc = acc_all + wave * DP;
   // diagnostic build only (DIAG & 32): cycles per loop segment
   uint64_t seg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = 0;
 #define BM25_STAMP(k)                                                           \
@@ -762,7 +776,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   const uint32_t lo = (uint32_t)(grp * per);
   const int32_t ngi = (int32_t)max<int64_t>(0, min<int64_t>(nitems, lo + per) - lo);
   if (ngi == 0) return;  // wave-uniform; no barriers in this kernel
-  const int32_t cm = (int32_t)((blockIdx.x >> 3) * kWaves + wave) % kClaimM;
+  const int32_t cm = (int32_t)((blockIdx.x >> 3) * kWaves + wave) % claim_m;
   int32_t* ctr = wctr + (grp * kClaimM + cm) * kCtrStride;
   const int tl = min(lane_id(), T - 1);
   const PostingRsrc pr = posting_rsrc(a);
@@ -789,7 +803,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
       c.tile = tile_of32<PH>((uint32_t)c.ti, (uint32_t)P);
       return c;
     }
-    const int64_t b = ((int64_t)uniform(pending) * kClaimM + cm) * kClaimCH;
+    const int64_t b = ((int64_t)uniform(pending) * claim_m + cm) * claim_ch;
     if (b >= ngi) {
       c.rit = c.end = ngi;
       return c;
@@ -797,7 +811,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     pending = claim();
     Cursor n;
     n.rit = (int32_t)b;
-    n.end = (int32_t)min<int64_t>(ngi, b + kClaimCH);
+    n.end = (int32_t)min<int64_t>(ngi, b + claim_ch);
     const uint32_t it = lo + (uint32_t)b;
     n.ti = (int32_t)(it / (uint32_t)nq);
     n.qi = (int32_t)(it - (uint32_t)n.ti * (uint32_t)nq);
@@ -816,6 +830,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
   Cursor cD = next(c0);
   if (cD.rit >= ngi) return;
   zero_acc<S>(acc);
+  acc[D + lane_id()] = 0.f;
   Cursor cC = next(cD), cB = next(cC), cA = next(cB);
   // prologue: item 0's first rows, item 1's bounds, item 2's terms
   int32_t tmD = terms_of(cD), tmC = terms_of(cC), tmB = terms_of(cB);
@@ -847,8 +862,8 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     BM25_STAMP(1);
     // (5) item n: adds in row order, then selection
     const int64_t tile = cD.tile;
-    add_rows<DIAG>(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ));
-    if (nrD > kJ) add_rows<DIAG>(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ));
+    add_rows<S, DIAG>(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ));
+    if (nrD > kJ) add_rows<S, DIAG>(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ));
     if (nrD > 2 * kJ) {  // heavy item: the remaining rows, block j + kJ issued before block j's adds
       const Desc dD = load_desc(a, tmD, tile);
       Rows t = rD;
@@ -865,7 +880,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
           if ((jn & 63) == 0) tn = make_rows(dD, T, jn);
           issue_rows(pr, tn, (int)(jn & 63), ltZ, vZ);
         }
-        add_rows<DIAG>(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ));
+        add_rows<S, DIAG>(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ));
         t = tn;
 #pragma unroll
         for (int i = 0; i < kJ; ++i) {
@@ -879,7 +894,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_pipe_kernel(
     if (DIAG & 4) {  // ablation: no selection
       zero_acc<S>(acc);
     } else if (PH == kRest && nrD <= 2 * kJ && (uint32_t)(thD >> 32) > score_key(0.f)) {
-      emit_sparse(acc, rD, ltD, ltX, nrD, tile, S, thD, list + (int64_t)cD.qi * C,
+      emit_sparse(acc, ltD, ltX, nrD, tile, S, thD, list + (int64_t)cD.qi * C,
                   list_cnt + cD.qi, C);
     } else if (PH == kRest) {
       emit_rest<S>(acc, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
@@ -1287,11 +1302,11 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
 }
 
 // Sampling stride: every P-th tile is a sample tile; P is the largest power of
-// two <= BM25_SAMPLE_P (default 8) whose sample still yields >= 2k candidates
+// two <= BM25_SAMPLE_P (default 16) whose sample still yields >= 2k candidates
 // (P = 1: one exact pass, no threshold).
 int sample_stride(int64_t ntiles, int k) {
   const char* e = getenv("BM25_SAMPLE_P");
-  const int pmax = e ? atoi(e) : 8;
+  const int pmax = e ? atoi(e) : 16;
   for (int P = 64; P >= 2; P >>= 1) {
     if (P > pmax) continue;
     const int64_t nS = (ntiles + P - 1) / P;
@@ -1318,6 +1333,18 @@ static bool use_pipe(const DevIndex& ix, int64_t T) {
   return !off && T >= 1 && T <= kGroup && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
 }
 
+// Item-claim geometry (BM25_CLAIM_CH / BM25_CLAIM_M override, for tuning).
+static int32_t claim_ch() {
+  const char* e = getenv("BM25_CLAIM_CH");
+  const int v = e ? atoi(e) : kClaimCH;
+  return v >= 1 && v <= 4096 ? v : kClaimCH;
+}
+static int32_t claim_m() {
+  const char* e = getenv("BM25_CLAIM_M");
+  const int v = e ? atoi(e) : 4;
+  return v >= 1 && v <= kClaimM ? v : 4;
+}
+
 // Diagnostic builds (BM25_ABLATE, dev only): 1 = no adds, 4 = no selection,
 // 5 = neither, 32 = s_memtime segment stamps of the REST kernel, printed to
 // stderr per launch.
@@ -1336,7 +1363,7 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
   hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG>), dim3((unsigned)grid),
                      dim3(64 * kWaves), 0, st, args_of(ix), q, (int32_t)T, sg.P, sg.nq_host,
                      sg.nq_dev, sg.qmap, ws.theta, ws.cand, ws.list, ws.list_cnt, ws.list_cap,
-                     ws.wctr, stamps);
+                     ws.wctr, claim_ch(), claim_m(), stamps);
   if ((DIAG & 32) && PH == kRest) {
     std::vector<uint64_t> h(8 * grid * kWaves);
     hipStreamSynchronize(st);
