@@ -303,7 +303,7 @@ __device__ __forceinline__ void emit_above(const float (&fv)[(1 << S) / 64], int
   // pass for docs < tie
   const int lim = (int)max<int64_t>(-1, min<int64_t>(D, n_docs - base));
   const int tie = (int)max<int64_t>(
-      -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base));
+      -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base + 1));
   float mx = fv[0];
 #pragma unroll
   for (int e = 1; e < E; ++e) mx = fmaxf(mx, fv[e]);
@@ -412,7 +412,7 @@ __device__ __forceinline__ void emit_rest(float* acc, int64_t tile, int64_t n_do
   // pass for docs < tie
   const int lim = (int)max<int64_t>(-1, min<int64_t>(D, n_docs - base));
   const int tie = (int)max<int64_t>(
-      -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base));
+      -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base + 1));
 #pragma unroll 1
   for (int j0 = 0; j0 < D / 256; j0 += 2) {  // not unrolled: 8 entries live at a time
     const float4 f0 = a4[j0 * 64 + lane], f1 = a4[(j0 + 1) * 64 + lane];
@@ -448,18 +448,19 @@ __device__ __forceinline__ void emit_rest(float* acc, int64_t tile, int64_t n_do
   }
 }
 
+// Tiles of a phase: SAMPLE visits every P-th tile, ALL and REST every tile.
 template <int PH>
 __device__ __forceinline__ int64_t tile_of(int64_t ti, int P) {
-  if (PH == kAll) return ti;
-  if (PH == kSample) return ti * P;
-  return (ti / (P - 1)) * P + (ti % (P - 1)) + 1;
+  return PH == kSample ? ti * P : ti;
 }
 template <int PH>
 __device__ __forceinline__ int32_t tile_of32(uint32_t ti, uint32_t P) {
-  if (PH == kAll) return (int32_t)ti;
-  if (PH == kSample) return (int32_t)(ti * P);
-  const uint32_t g = ti / (P - 1u);
-  return (int32_t)(g * P + (ti - g * (P - 1u)) + 1u);
+  return (int32_t)(PH == kSample ? ti * P : ti);
+}
+// Keys per candidate tile of a phase's cand array: 1 (SAMPLE) or kTileM (ALL).
+template <int PH>
+constexpr int cand_per_tile() {
+  return PH == kSample ? 1 : kTileM;
 }
 
 // ---------------------------------------------------------------------------
@@ -650,7 +651,7 @@ __device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ]
   const int64_t base = tile << S;
   // ties pass for tile-local docs < tie (clamped to [-1, 2^S])
   const int tie = (int)max<int64_t>(
-      -1, min<int64_t>(1 << S, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base));
+      -1, min<int64_t>(1 << S, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base + 1));
   uint32_t pm = 0;
 #pragma unroll
   for (int j = 0; j < 2 * kJ; ++j) {
@@ -685,6 +686,46 @@ __device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ]
 // tiles than L2 holds.
 // (kClaimCH, kClaimM, kCtrStride: bm25mi_internal.h)
 
+// SAMPLE items of at most 2 kJ rows: the best key among the touched docs with
+// a positive sum (0 if none), read and cleared as in emit_sparse.  Any real
+// document's key serves theta (a lower bound of the k-th key), so ignoring the
+// untouched docs and non-positive sums is safe.
+__device__ __forceinline__ uint64_t best_sparse(float* acc, const uint32_t (&l0)[kJ],
+                                                const uint32_t (&l1)[kJ], uint32_t nr,
+                                                int64_t tile, int S) {
+  uint32_t bk = 0, bd = 0;
+#pragma unroll
+  for (int j = 0; j < 2 * kJ; ++j) {
+    if ((uint32_t)j < nr) {
+      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
+      const float x = acc[l];
+      acc[l] = 0.f;
+      const uint32_t key = x > 0.f ? score_key(x) : 0u;
+      bd = key > bk ? l : bd;
+      bk = key > bk ? key : bk;
+    }
+  }
+  const uint32_t wm = wave_max_u32(bk);
+  if (wm == 0) return 0ull;
+  const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk == wm ? 0xFFFFFFFFu - bd : 0u);
+  return ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)((tile << S) + doc));
+}
+
+// Dense form: the tile's best key over every accumulator (ties: smallest
+// doc), then the accumulators are cleared.
+template <int S>
+__device__ __forceinline__ uint64_t best_dense(float* acc, int64_t tile, int64_t n_docs) {
+  const int64_t base = tile << S;
+  const int lim = (int)min<int64_t>(1 << S, n_docs - base);
+  uint32_t bk, bd;
+  lane_best<S>(acc, lim, bk, bd);
+  zero_acc<S>(acc);
+  const uint32_t wm = wave_max_u32(bk);
+  if (wm == 0) return 0ull;
+  const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk == wm ? 0xFFFFFFFFu - bd : 0u);
+  return ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc));
+}
+
 struct Cursor {  // XCD-relative item rit = (ti, qi) and its tile; end = its chunk's end
   int32_t rit, end, ti, qi, tile;
 };
@@ -708,8 +749,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
   float* acc = acc_all + wave * D;
   const int64_t nq = sg.nq_dev ? (int64_t)*sg.nq_dev : (int64_t)sg.nq_host;
   const int P = sg.P;
-  const int64_t nS = (a.ntiles + P - 1) / P;
-  const int64_t nt = PH == kAll ? a.ntiles : (PH == kSample ? nS : a.ntiles - nS);
+  const int64_t nt = PH == kSample ? (a.ntiles + P - 1) / P : a.ntiles;
   const int64_t nitems = nt * nq;
   const int64_t per = (nitems + 7) >> 3;
   const int64_t grp = blockIdx.x & 7;
@@ -730,7 +770,8 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
     if (PH == kRest)
       emit_above<S>(fv, tile, a.n_docs, theta[qi], list + qi * C, list_cnt + qi, C);
     else
-      select_top<S>(fv, tile, a.n_docs, kTileM, cand + (qi * nt + ti) * kTileM);
+      select_top<S>(fv, tile, a.n_docs, cand_per_tile<PH>(),
+                    cand + (qi * nt + ti) * cand_per_tile<PH>());
   }
 }
 
@@ -768,8 +809,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
   }
   BM25_STAMP(7);
   const int32_t nq = QMAP ? *nq_dev : nq_host;
-  const int32_t nS = (int32_t)((a.ntiles + P - 1) / P);
-  const int32_t nt = PH == kAll ? (int32_t)a.ntiles : (PH == kSample ? nS : (int32_t)a.ntiles - nS);
+  const int32_t nt = PH == kSample ? (int32_t)((a.ntiles + P - 1) / P) : (int32_t)a.ntiles;
   const int64_t nitems = (int64_t)nt * nq;
   const int64_t per = (nitems + 7) >> 3;
   const int grp = (int)(blockIdx.x & 7);
@@ -898,6 +938,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
                   list_cnt + cD.qi, C);
     } else if (PH == kRest) {
       emit_rest<S>(acc, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
+    } else if (PH == kSample) {
+      const uint64_t key = nrD <= 2 * kJ ? best_sparse(acc, ltD, ltX, nrD, tile, S)
+                                         : best_dense<S>(acc, tile, a.n_docs);
+      if (lane_id() == 0) cand[(int64_t)cD.qi * nt + cD.ti] = key;
     } else {
       select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + ((int64_t)cD.qi * nt + cD.ti) * kTileM);
     }
@@ -1190,15 +1234,25 @@ struct SrcLists {
   }
 };
 
-// theta[q] = k-th best key among the sample tiles' candidates: k real
-// documents score at least this, so it is a lower bound of the final k-th key.
+// theta[q] = k-th best key among the sample tiles' keys: k real documents
+// score at least this, so it is a lower bound of the final k-th key.  A query
+// with fewer than k sample keys (a sample item reports no key when none of its
+// touched docs has a positive sum) gets no threshold: theta = all ones (a NaN
+// score: no REST key passes) and its list is marked overflowed, which sends it
+// to the exact fallback stage.
 __global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restrict__ cand,
                                                          int64_t nS, int32_t k,
-                                                         uint64_t* __restrict__ theta) {
+                                                         uint64_t* __restrict__ theta,
+                                                         int32_t* __restrict__ list_cnt,
+                                                         int32_t C) {
   __shared__ uint64_t keys[kMergeP];
   const int64_t q = blockIdx.x;
-  topk_of(SrcFirst{cand + q * nS * kTileM}, nS * kTileM, k, keys);
-  if (threadIdx.x == 0) theta[q] = keys[k - 1];
+  topk_of(SrcFirst{cand + q * nS}, nS, k, keys);
+  if (threadIdx.x == 0) {
+    const uint64_t t = keys[k - 1];
+    theta[q] = t != 0ull ? t : ~0ull;
+    if (t == 0ull) list_cnt[q] = C + 1;
+  }
 }
 
 __device__ __forceinline__ int64_t stage_nq(const Stage& sg) {
@@ -1310,7 +1364,7 @@ int sample_stride(int64_t ntiles, int k) {
   for (int P = 64; P >= 2; P >>= 1) {
     if (P > pmax) continue;
     const int64_t nS = (ntiles + P - 1) / P;
-    if (ntiles >= 2 * P && nS * kTileM >= 2 * (int64_t)k) return P;
+    if (ntiles >= 2 * P && nS >= 2 * (int64_t)k) return P;
   }
   return 1;
 }
@@ -1407,7 +1461,7 @@ static Stage main_stage(const DevIndex& ix, int64_t Q, int P, const Workspace& w
   Stage sg{};
   sg.cand = ws.cand;
   sg.P = P;
-  sg.nt = (ix.ntiles + P - 1) / P;
+  sg.nt = P > 1 ? 0 : ix.ntiles;  // sampled search: the merge reads the list only
   sg.nq_host = (int32_t)Q;
   if (P > 1) {
     sg.theta = ws.theta;
@@ -1443,8 +1497,8 @@ static void score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, 
   }
   hipMemsetAsync(ws.list_cnt, 0, sizeof(int32_t) * Q, st);
   launch_wave<S, kSample>(ix, q, T, sg, ws, st);
-  hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, ws.cand, sg.nt,
-                     (int32_t)k, ws.theta);
+  hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, ws.cand,
+                     (ix.ntiles + P - 1) / P, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap);
   launch_wave<S, kRest>(ix, q, T, sg, ws, st);
 }
 
@@ -1465,7 +1519,7 @@ static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k,
   const int64_t maxflag = maxflag_for(k, sg.nt);
   hipLaunchKernelGGL(merge_first_kernel, dim3((unsigned)sg.nq_host), dim3(kMergeNT), 0, st, sg,
                      (int32_t)k, maxflag, ix.doc_offset, ws, docs, scores);
-  if (k > kTileM) {
+  if (k > kTileM && sg.nt > 0) {  // tiles with exact top-4 candidates may need a rescore
     hipLaunchKernelGGL(rescore_kernel<S>, dim3(256), dim3(kRescoreNT), 0, st, args_of(ix), q,
                        (int32_t)T, (int32_t)k, maxflag, sg, ws);
     hipLaunchKernelGGL(merge_final_kernel, dim3((unsigned)sg.nq_host), dim3(kMergeNT), 0, st, sg,
