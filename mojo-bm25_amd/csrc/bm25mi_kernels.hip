@@ -571,57 +571,85 @@ __device__ __forceinline__ void issue_rows(const PostingRsrc& pr, const Rows& R,
   }
 }
 
-// The first n (uniform) of the loaded rows, in order.  Per row: ds_read,
-// add, ds_write (an LDS float atomic does the same add at ~2.5x the cost on
-// gfx950: 23.8 vs 10.9 ms for the config-3 score pass).  A run of rows of one
-// term holds distinct docs, so its reads are issued together and its writes
-// after one wait; before the first read of the next term every pending write
-// is issued, and the LDS executes a wave's instructions in order, so each
-// doc's adds stay in query-term order.
-//
-// Lanes past a row's postings are redirected to the lane's own trash slot
-// (acc[2^S + lane], always 0) with a zero score, so every LDS access runs
-// unmasked: no exec-mask branches, and the compiler keeps its lgkmcnt waits
-// counted.  The redirected slots are written back into ld for the sparse
-// emission.
-template <int S, int DIAG>
-__device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0, uint32_t (&ld)[kJ],
-                                         float (&v)[kJ], uint32_t n) {
+// Rows of a block processed: the first 4 or all kJ (a uniform choice from the
+// block's row count n); rows past n in the processed range are all-trash.
+__device__ __forceinline__ int rows_done(uint32_t n) { return n == 0 ? 0 : (n <= kJ / 2 ? kJ / 2 : kJ); }
+
+// Read-add-write of NR loaded rows, in order.  Lanes past a row's postings
+// are redirected to the lane's own trash slot (acc[2^S + lane], always 0) with
+// a zero score, so every LDS access runs unmasked (no exec-mask branches; the
+// compiler keeps its lgkmcnt waits counted); the redirected slots are written
+// back into ld for the sparse emission.  Each row is read, added and written
+// back before the next row of ANOTHER term is read — the LDS executes a
+// wave's instructions in order, so each doc's adds stay in query-term order
+// (scipy csc_matvec's sequence) — while the next row of the SAME term (distinct
+// docs) is read one row ahead.  (An LDS float atomic per row, ds_add_f32, ran
+// the config-3 score pass 4.7x slower: 24.8 vs 5.3 ms.)
+template <int S, int NR>
+__device__ __forceinline__ void rmw_rows(float* acc, const Rows& R, int j0, uint32_t (&ld)[kJ],
+                                         float (&v)[kJ]) {
   const uint32_t lane = lane_id();
   const uint32_t trash = (1u << S) + lane;
 #pragma unroll
-  for (int j = 0; j < kJ; ++j) {
-    if ((uint32_t)j < n) {
-      const bool m = lane < lane_u32(R.cnt, j0 + j);
-      ld[j] = m ? ld[j] : trash;
-      v[j] = m ? v[j] : 0.f;
-    }
+  for (int j = 0; j < NR; ++j) {
+    const bool m = lane < lane_u32(R.cnt, j0 + j);
+    ld[j] = m ? ld[j] : trash;
+    v[j] = m ? v[j] : 0.f;
   }
+  // bit j of bm: row j0 + j starts a new term
+  const uint32_t tprev = (uint32_t)__shfl_up((int)R.term, 1, 64);
+  const uint32_t bm = (uint32_t)(__ballot(R.term != tprev) >> j0);
+  float x[NR];
+  x[0] = acc[ld[0]];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const bool same = j + 1 < NR && !((bm >> (j + 1)) & 1u);
+    if (same) x[j + 1] = acc[ld[j + 1]];
+    acc[ld[j]] = x[j] + v[j];
+    if (j + 1 < NR && !same) x[j + 1] = acc[ld[j + 1]];
+  }
+}
+
+template <int S, int DIAG>
+__device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0, uint32_t (&ld)[kJ],
+                                         float (&v)[kJ], uint32_t n) {
   if (DIAG & 1) {  // ablation: consume the loads, no adds
 #pragma unroll
     for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
     return;
   }
-  float x[kJ];
-  uint32_t tprev = ~0u;
-  int f = 0;  // rows [f, j) read, not yet written
+  const int nr = rows_done(n);
+  if (nr == kJ)
+    rmw_rows<S, kJ>(acc, R, j0, ld, v);
+  else if (nr > 0)
+    rmw_rows<S, kJ / 2>(acc, R, j0, ld, v);
+}
+
+// The final sums of an item's processed rows (add_rows' ranges of the D and
+// X blocks, nr rows in all), each read once and cleared; x = 0 elsewhere.
+__device__ __forceinline__ void read_clear(float* acc, const uint32_t (&l0)[kJ],
+                                           const uint32_t (&l1)[kJ], uint32_t nr,
+                                           float (&x)[2 * kJ]) {
+  const uint32_t n0 = min(nr, (uint32_t)kJ), n1 = nr > (uint32_t)kJ ? nr - kJ : 0u;
+  const int r0 = rows_done(n0), r1 = rows_done(n1);
+#pragma unroll
+  for (int j = 0; j < 2 * kJ; ++j) x[j] = 0.f;
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
-    if ((uint32_t)j < n) {
-      const uint32_t tj = lane_u32(R.term, j0 + j);
-      if (tj != tprev) {  // a new term: the earlier rows' writes go first
-#pragma unroll
-        for (int i = 0; i < j; ++i)
-          if (i >= f) acc[ld[i]] = x[i] + v[i];
-        f = j;
-      }
-      tprev = tj;
-      x[j] = acc[ld[j]];
+    if (r0 > 0 && (j < kJ / 2 || r0 == kJ)) {
+      x[j] = acc[l0[j]];
+      acc[l0[j]] = 0.f;
     }
   }
+  if (r1 > 0) {
 #pragma unroll
-  for (int i = 0; i < kJ; ++i)
-    if (i >= f && (uint32_t)i < n) acc[ld[i]] = x[i] + v[i];
+    for (int j = 0; j < kJ; ++j) {
+      if (j < kJ / 2 || r1 == kJ) {
+        x[kJ + j] = acc[l1[j]];
+        acc[l1[j]] = 0.f;
+      }
+    }
+  }
 }
 
 // REST emission from the item's own postings (items of at most 2 kJ rows,
@@ -638,15 +666,7 @@ __device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ]
                                             int32_t* __restrict__ cnt, int32_t C) {
   const uint32_t lane = lane_id();
   float x[2 * kJ];
-#pragma unroll
-  for (int j = 0; j < 2 * kJ; ++j) {
-    x[j] = 0.f;
-    if ((uint32_t)j < nr) {
-      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
-      x[j] = acc[l];
-      acc[l] = 0.f;
-    }
-  }
+  read_clear(acc, l0, l1, nr, x);
   const float th = key_score((uint32_t)(theta >> 32));
   const int64_t base = tile << S;
   // ties pass for tile-local docs < tie (clamped to [-1, 2^S])
@@ -693,17 +713,15 @@ __device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ]
 __device__ __forceinline__ uint64_t best_sparse(float* acc, const uint32_t (&l0)[kJ],
                                                 const uint32_t (&l1)[kJ], uint32_t nr,
                                                 int64_t tile, int S) {
+  float x[2 * kJ];
+  read_clear(acc, l0, l1, nr, x);
   uint32_t bk = 0, bd = 0;
 #pragma unroll
   for (int j = 0; j < 2 * kJ; ++j) {
-    if ((uint32_t)j < nr) {
-      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
-      const float x = acc[l];
-      acc[l] = 0.f;
-      const uint32_t key = x > 0.f ? score_key(x) : 0u;
-      bd = key > bk ? l : bd;
-      bk = key > bk ? key : bk;
-    }
+    const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
+    const uint32_t key = x[j] > 0.f ? score_key(x[j]) : 0u;
+    bd = key > bk ? l : bd;
+    bk = key > bk ? key : bk;
   }
   const uint32_t wm = wave_max_u32(bk);
   if (wm == 0) return 0ull;
