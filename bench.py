@@ -67,7 +67,7 @@ def load_traffic(path: str, config: str, shift: int):
         with open(path) as f:
             t = json.load(f)
         if t.get("config") == config and int(t.get("tile_shift", -1)) == shift:
-            return t.get("hbm_bytes_per_launch")
+            return t
     except (OSError, ValueError):
         pass
     return None
@@ -87,7 +87,8 @@ def main():
 
     import torch
     from bm25mi import synth
-    from bm25mi.index import GpuIndex, merge_topk_device
+    from bm25mi.index import GpuIndex
+    from bm25mi.dist import gpu_merge, sharded_topk
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -117,19 +118,13 @@ def main():
     dq = torch.from_numpy(queries).to(dev)
     d_docs = torch.empty((Q, k), dtype=torch.int32, device=dev)
     d_scores = torch.empty((Q, k), dtype=torch.float32, device=dev)
-    if world > 1:
-        g_docs = torch.empty((world, Q, k), dtype=torch.int32, device=dev)
-        g_scores = torch.empty((world, Q, k), dtype=torch.float32, device=dev)
-        m_docs = torch.empty((Q, k), dtype=torch.int32, device=dev)
-        m_scores = torch.empty((Q, k), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    merge = gpu_merge(local, stream)
 
     def step():
         index.search_device(dq, k, d_docs, d_scores, stream)
-        if world > 1:
-            dist.all_gather_into_tensor(g_docs, d_docs)
-            dist.all_gather_into_tensor(g_scores, d_scores)
-            merge_topk_device(local, g_docs, g_scores, world, Q, k, m_docs, m_scores, stream)
+        if world > 1:  # RCCL all-gather of the [Q, k] lists + HIP merge (bm25mi.dist)
+            sharded_topk(d_docs, d_scores, merge)
 
     for _ in range(args.warmup):
         step()
@@ -206,7 +201,9 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic,
+                "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                "traffic_source": (f"profiles/traffic.json: {traffic.get('method')}; "
+                                   f"L2 hit rate {traffic.get('l2_hit_rate')}") if traffic else None,
                 "kernel": "score_tiles",
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,

@@ -1,0 +1,80 @@
+"""Doc-sharded search across ranks.
+
+One process per GPU.  Rank r owns the contiguous document range
+``synth.shard_bounds(N, W, r)`` as an independent index whose ``doc_offset``
+is the global id of its first document, and searches the whole (replicated)
+query batch on it.  The only exchange of the path is this one: every rank's
+[Q, k] top-k list (global doc ids + scores) is all-gathered into [W, Q, k]
+(RCCL over xGMI with the ``nccl`` backend) and merged by the same
+(score desc, doc asc) rule, so the result is exactly the single-index top-k.
+
+The reference has no multi-device path (``DEVICE_ID = 0`` at
+main.py:205); this module is the build's only collective.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+# merge(g_docs [W,Q,k] int32, g_scores [W,Q,k] f32) -> (docs [Q,k], scores [Q,k])
+MergeFn = Callable[[torch.Tensor, torch.Tensor], Tuple[torch.Tensor, torch.Tensor]]
+
+
+def shard_bounds(n_docs: int, world: int, rank: int, align: int = 2048) -> Tuple[int, int]:
+    """Contiguous doc range [lo, hi) of ``rank``: an even split with inner
+    boundaries rounded to multiples of ``align`` (the 2048-doc LDS tile, so no
+    shard carries a partial tile except the last; synth.shard_bounds uses the
+    generator's 16384-doc chunks, a multiple of it)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad shard {rank} of {world}")
+
+    def b(r: int) -> int:
+        if r >= world:
+            return int(n_docs)
+        x = (int(n_docs) * r) // world
+        return min(int(n_docs), (x + align // 2) // align * align)
+
+    return b(rank), b(rank + 1)
+
+
+def all_gather_lists(docs: torch.Tensor, scores: torch.Tensor,
+                     group: Optional[dist.ProcessGroup] = None
+                     ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All ranks' [Q, k] lists -> [W, Q, k] (rank-major), on every rank."""
+    world = dist.get_world_size(group)
+    g_docs = torch.empty((world,) + tuple(docs.shape), dtype=docs.dtype, device=docs.device)
+    g_scores = torch.empty((world,) + tuple(scores.shape), dtype=scores.dtype,
+                           device=scores.device)
+    if dist.get_backend(group) == "gloo":  # no into-tensor form on gloo
+        dist.all_gather(list(g_docs.unbind(0)), docs.contiguous(), group=group)
+        dist.all_gather(list(g_scores.unbind(0)), scores.contiguous(), group=group)
+    else:
+        dist.all_gather_into_tensor(g_docs, docs.contiguous(), group=group)
+        dist.all_gather_into_tensor(g_scores, scores.contiguous(), group=group)
+    return g_docs, g_scores
+
+
+def sharded_topk(docs: torch.Tensor, scores: torch.Tensor, merge: MergeFn,
+                 group: Optional[dist.ProcessGroup] = None
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """This rank's [Q, k] list (global doc ids) -> the global [Q, k] top-k."""
+    if dist.get_world_size(group) == 1:
+        return docs, scores
+    g_docs, g_scores = all_gather_lists(docs, scores, group)
+    return merge(g_docs, g_scores)
+
+
+def gpu_merge(device: int, stream=None) -> MergeFn:
+    """The HIP merge (bm25_merge_topk_device) as a MergeFn, on ``stream``."""
+    from .index import merge_topk_device
+
+    def merge(g_docs: torch.Tensor, g_scores: torch.Tensor):
+        W, Q, k = g_docs.shape
+        out_d = torch.empty((Q, k), dtype=torch.int32, device=g_docs.device)
+        out_s = torch.empty((Q, k), dtype=torch.float32, device=g_docs.device)
+        merge_topk_device(device, g_docs, g_scores, W, Q, k, out_d, out_s, stream)
+        return out_d, out_s
+
+    return merge
