@@ -128,6 +128,33 @@ int bm25_merge_topk_device(int device, const int32_t* d_docs,
                            void* stream);
 
 /*
+ * Doc-sharded index over several devices of ONE process.
+ * The reference is single-device (DEVICE_ID = 0, main.py:205, graph.py:95);
+ * this is the build's multi-GPU form of BM25v.index / BM25v.search
+ * (bm25_native.py:59-103) for callers that own all local GPUs.  The multi-
+ * process form (one rank per GPU, RCCL all-gather) is bm25mi.dist + the
+ * *_device calls above.
+ *   bm25_sharded_create: same CSC arguments as bm25_index_create; documents
+ *     are split into n_dev contiguous, 2048-doc-aligned ranges, shard s on
+ *     devices[s] (a device may be listed more than once).
+ *   bm25_sharded_search: same contract as bm25_search; each shard searches on
+ *     its own stream, the per-shard [Q, k] lists are copied to devices[0]
+ *     (peer copies) and merged there; the result equals a single-index search.
+ *     Errors as bm25_search, plus EINVAL when k exceeds a shard's documents.
+ *   bm25_sharded_info: shard count and [lo, hi) doc ranges (arrays of n_dev).
+ */
+typedef struct bm25_sharded bm25_sharded;
+
+int bm25_sharded_create(int n_dev, const int* devices, int64_t n_docs, int64_t n_terms,
+                        int64_t nnz, const void* indptr, int indptr_is_i64,
+                        const int32_t* indices, const float* data, bm25_sharded** out);
+int bm25_sharded_search(bm25_sharded* s, const int32_t* queries, int64_t Q, int64_t T,
+                        int32_t k, int32_t* out_docs, float* out_scores);
+int bm25_sharded_info(const bm25_sharded* s, int64_t* n_shards, int64_t* shard_lo,
+                      int64_t* shard_hi);
+int bm25_sharded_destroy(bm25_sharded* s);
+
+/*
  * Timing of the score pass (sample + theta + rest score kernels, the HBM
  * bound part of a search), measured with HIP events recorded on the search
  * stream around it in every search while enabled.

@@ -16,7 +16,7 @@ Deliberate differences:
 from __future__ import annotations
 
 import logging
-from typing import Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 import scipy.sparse as sp
@@ -56,6 +56,22 @@ class BM25v:
         if self._gpu is not None:
             self._gpu.close()
         self._gpu = GpuIndex.from_csc(doc_toks, device=self.device)
+
+    @classmethod
+    def from_bm25s(cls, path: str, device: int = 0, k1: Optional[float] = None,
+                   b: Optional[float] = None) -> "BM25v":
+        """A BM25v over a bm25s index directory (indptr/indices/data
+        .csc.index.npy + params.index.json, bm25_test.py:35-42), with doc
+        lengths of ones (bm25s does not store them; unused for scoring)."""
+        from bm25mi.bm25s_io import load_bm25s
+        ix = load_bm25s(path)
+        m = cls(k1=ix.params.get("k1", 1.5) if k1 is None else k1,
+                b=ix.params.get("b", 0.75) if b is None else b, device=device)
+        m.vocab = ix.vocab
+        n = ix.num_docs
+        m.index(sp.csc_matrix((ix.data, ix.indices, ix.indptr), shape=(n, ix.n_terms)),
+                np.ones(n, np.float32))
+        return m
 
     def search(self, queries, top_k: int = 100) -> Tuple[np.ndarray, np.ndarray]:
         """bm25_native.py:76-103: sorted top-k doc ids (int32) and scores (f32)."""

@@ -59,6 +59,11 @@ _SIGS = {
     "bm25_profile_enable": ([_P, ctypes.c_int], ctypes.c_int),
     "bm25_profile_read": ([_P, _PD, _PI64, _PD, _PI64, _PI64], ctypes.c_int),
     "bm25_search_stats": ([_P, _PI64, _PI64], ctypes.c_int),
+    "bm25_sharded_create": ([ctypes.c_int, _P, _I64, _I64, _I64, _P, ctypes.c_int, _P, _P,
+                             ctypes.POINTER(_P)], ctypes.c_int),
+    "bm25_sharded_search": ([_P, _P, _I64, _I64, _I32, _P, _P], ctypes.c_int),
+    "bm25_sharded_info": ([_P, _PI64, _P, _P], ctypes.c_int),
+    "bm25_sharded_destroy": ([_P], ctypes.c_int),
 }
 for _name, (_args, _res) in _SIGS.items():
     _f = getattr(lib, _name)

@@ -153,5 +153,60 @@ def merge_topk_device(device: int, d_docs, d_scores, W: int, Q: int, k: int, d_o
                                      ctypes.c_void_p(s)))
 
 
+class ShardedIndex:
+    """A CSC index doc-sharded over several GPUs of this process
+    (bm25_sharded_* in include/bm25mi.h): ``search`` has GpuIndex.search's
+    contract and returns the single-index result."""
+
+    def __init__(self, indptr, indices, data, n_docs: int, devices):
+        devices = [int(d) for d in devices]
+        if not devices:
+            raise ValueError("need at least one device")
+        indptr = np.asarray(indptr)
+        ip_i64 = indptr.dtype == np.int64 or indptr[-1] > np.iinfo(np.int32).max
+        ip = np.ascontiguousarray(indptr, dtype=np.int64 if ip_i64 else np.int32)
+        ix = np.ascontiguousarray(indices, dtype=np.int32)
+        dt = np.ascontiguousarray(data, dtype=np.float32)
+        devs = np.asarray(devices, np.int32)
+        self.n_docs = int(n_docs)
+        self.n_terms = int(ip.size - 1)
+        self._h = None
+        h = ctypes.c_void_p()
+        check(lib.bm25_sharded_create(len(devices), _ptr(devs), self.n_docs, self.n_terms,
+                                      int(ip[-1]), _ptr(ip), int(ip_i64), _ptr(ix), _ptr(dt),
+                                      ctypes.byref(h)))
+        self._h = h
+
+    def shards(self):
+        n = ctypes.c_int64()
+        check(lib.bm25_sharded_info(self._h, ctypes.byref(n), None, None))
+        lo = np.zeros(n.value, np.int64)
+        hi = np.zeros(n.value, np.int64)
+        check(lib.bm25_sharded_info(self._h, ctypes.byref(n), _ptr(lo), _ptr(hi)))
+        return list(zip(lo.tolist(), hi.tolist()))
+
+    def search(self, queries: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        q = np.ascontiguousarray(queries, dtype=np.int32)
+        if q.ndim != 2:
+            raise ValueError("queries must be a 2-D [Q, T] int32 array")
+        Q, T = q.shape
+        k = int(k)
+        docs = np.zeros((Q, max(k, 0)), np.int32)
+        scores = np.zeros((Q, max(k, 0)), np.float32)
+        check(lib.bm25_sharded_search(self._h, _ptr(q), Q, T, k, _ptr(docs), _ptr(scores)))
+        return docs, scores
+
+    def close(self) -> None:
+        if self._h is not None:
+            lib.bm25_sharded_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def device_count() -> int:
     return _capi.device_count()

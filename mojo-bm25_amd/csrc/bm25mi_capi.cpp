@@ -473,3 +473,217 @@ int bm25_search_stats(bm25_index* h, int64_t* rescored_tiles, int64_t* fallback_
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Doc-sharded index over several devices of one process:
+// shard s owns the tile-aligned doc range [lo_s, hi_s) as an ordinary index
+// (doc_offset = lo_s) on devices[s]; a search runs every shard on its own
+// stream, copies the per-shard [Q, k] lists to shard 0's device (peer copies
+// ordered by events) and merges them there with merge_lists_kernel — the same
+// (score desc, doc asc) rule, so the result equals a single-index search.
+// ---------------------------------------------------------------------------
+struct bm25_sharded {
+  std::vector<bm25_index*> shards;
+  std::vector<int64_t> lo, hi;
+  std::vector<hipEvent_t> done;  // per shard: its search finished
+  int64_t n_docs = 0, n_terms = 0;
+  int32_t* g_docs = nullptr;     // [W][Q][k] on shard 0's device
+  float* g_scores = nullptr;
+  int32_t* m_docs = nullptr;     // [Q][k]
+  float* m_scores = nullptr;
+  int64_t cap_g = 0, cap_m = 0;
+  std::mutex mu;
+};
+
+namespace {
+
+int sharded_free(bm25_sharded* s) {
+  if (!s) return BM25_OK;
+  if (!s->shards.empty() && s->shards[0]) {
+    hipSetDevice(s->shards[0]->ix.device);
+    hipFree(s->g_docs);
+    hipFree(s->g_scores);
+    hipFree(s->m_docs);
+    hipFree(s->m_scores);
+  }
+  for (size_t i = 0; i < s->shards.size(); ++i) {
+    if (!s->shards[i]) continue;
+    hipSetDevice(s->shards[i]->ix.device);
+    if (i < s->done.size() && s->done[i]) hipEventDestroy(s->done[i]);
+    bm25_index_destroy(s->shards[i]);
+  }
+  delete s;
+  return BM25_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bm25_sharded_create(int n_dev, const int* devices, int64_t n_docs, int64_t n_terms,
+                        int64_t nnz, const void* indptr, int indptr_is_i64,
+                        const int32_t* indices, const float* data, bm25_sharded** out) {
+  if (!out) return fail(BM25_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (n_dev < 1 || !devices) return fail(BM25_EINVAL, "need at least one device");
+  if (n_docs < 0 || n_terms < 0 || nnz < 0) return fail(BM25_EINVAL, "negative size");
+  if (!indptr || (nnz > 0 && (!indices || !data))) return fail(BM25_EINVAL, "NULL CSC array");
+  std::vector<int64_t> ip(n_terms + 1);
+  for (int64_t t = 0; t <= n_terms; ++t)
+    ip[t] = indptr_is_i64 ? ((const int64_t*)indptr)[t] : (int64_t)((const int32_t*)indptr)[t];
+  if (ip[0] != 0 || ip[n_terms] != nnz)
+    return fail(BM25_EINVAL, "indptr must start at 0 and end at nnz");
+  for (int64_t t = 0; t < n_terms; ++t)
+    if (ip[t + 1] < ip[t]) return fail(BM25_EINVAL, "indptr decreases at column %lld", (long long)t);
+  bm25_sharded* s = new bm25_sharded();
+  s->n_docs = n_docs;
+  s->n_terms = n_terms;
+  const int64_t align = 2048;
+  auto bound = [&](int64_t r) -> int64_t {
+    if (r >= n_dev) return n_docs;
+    const int64_t x = n_docs * r / n_dev;
+    return std::min(n_docs, (x + align / 2) / align * align);
+  };
+  std::vector<int64_t> sip(n_terms + 1);
+  std::vector<int32_t> six;
+  std::vector<float> sdt;
+  for (int r = 0; r < n_dev; ++r) {
+    const int64_t lo = bound(r), hi = bound(r + 1);
+    // the shard's CSC: per column, the entries with lo <= doc < hi (columns are
+    // sorted; unsorted input is rejected by the shard's own build check)
+    sip[0] = 0;
+    for (int64_t t = 0; t < n_terms; ++t) {
+      const int32_t* b = indices + ip[t];
+      const int32_t* e = indices + ip[t + 1];
+      const int32_t* p0 = std::lower_bound(b, e, (int32_t)std::min<int64_t>(lo, INT32_MAX));
+      const int32_t* p1 = std::lower_bound(p0, e, (int32_t)std::min<int64_t>(hi, INT32_MAX));
+      sip[t + 1] = sip[t] + (p1 - p0);
+    }
+    six.resize(std::max<int64_t>(sip[n_terms], 1));
+    sdt.resize(std::max<int64_t>(sip[n_terms], 1));
+    for (int64_t t = 0; t < n_terms; ++t) {
+      const int32_t* b = indices + ip[t];
+      const int32_t* e = indices + ip[t + 1];
+      const int32_t* p0 = std::lower_bound(b, e, (int32_t)std::min<int64_t>(lo, INT32_MAX));
+      for (int64_t i = 0; i < sip[t + 1] - sip[t]; ++i) {
+        six[sip[t] + i] = p0[i] - (int32_t)lo;
+        sdt[sip[t] + i] = data[(p0 - indices) + i];
+      }
+    }
+    bm25_index* h = nullptr;
+    const int rc = bm25_index_create(devices[r], hi - lo, n_terms, sip[n_terms], sip.data(), 1,
+                                     six.data(), sdt.data(), lo, &h);
+    if (rc) {
+      const std::string msg = g_err;
+      sharded_free(s);
+      return fail(rc, "shard %d (device %d): %s", r, devices[r], msg.c_str());
+    }
+    s->shards.push_back(h);
+    s->lo.push_back(lo);
+    s->hi.push_back(hi);
+    hipEvent_t ev = nullptr;
+    hipSetDevice(devices[r]);
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      sharded_free(s);
+      return fail(BM25_EHIP, "hipEventCreate");
+    }
+    s->done.push_back(ev);
+  }
+  *out = s;
+  return BM25_OK;
+}
+
+int bm25_sharded_destroy(bm25_sharded* s) { return sharded_free(s); }
+
+int bm25_sharded_search(bm25_sharded* s, const int32_t* queries, int64_t Q, int64_t T,
+                        int32_t k, int32_t* out_docs, float* out_scores) {
+  if (!s) return fail(BM25_EINVAL, "NULL index");
+  if (Q < 0 || T < 0) return fail(BM25_EINVAL, "negative query shape");
+  if (k < 0) return fail(BM25_EINVAL, "negative dimensions are not allowed (top_k=%d)", k);
+  if (k > s->n_docs)
+    return fail(BM25_EINVAL, "kth(=%lld) out of bounds (%lld)", (long long)(s->n_docs - k),
+                (long long)s->n_docs);
+  if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%d exceeds the engine limit %d", k, kMaxK);
+  if (Q == 0 || k == 0) return BM25_OK;
+  if (T > 0 && !queries) return fail(BM25_EINVAL, "NULL queries");
+  if (!out_docs || !out_scores) return fail(BM25_EINVAL, "NULL output");
+  int64_t mx = 0;
+  for (int64_t i = 0; i < Q * T; ++i) mx = std::max<int64_t>(mx, queries[i]);
+  if (mx >= s->n_terms)
+    return fail(BM25_EINVAL,
+                "The maximum token ID in the query (%lld) is higher than the number of tokens in "
+                "the index.",
+                (long long)mx);
+  const int64_t W = (int64_t)s->shards.size();
+  for (int64_t r = 0; r < W; ++r)
+    if (s->hi[r] - s->lo[r] < k)
+      return fail(BM25_EINVAL, "top_k=%d exceeds the %lld documents of shard %lld", k,
+                  (long long)(s->hi[r] - s->lo[r]), (long long)r);
+  std::lock_guard<std::mutex> lk(s->mu);
+  bm25_index* h0 = s->shards[0];
+  const int64_t out = Q * (int64_t)k;
+  HIP_TRY(hipSetDevice(h0->ix.device), "hipSetDevice");
+  if (W * out > s->cap_g) {
+    hipFree(s->g_docs);
+    hipFree(s->g_scores);
+    s->g_docs = nullptr;
+    s->g_scores = nullptr;
+    HIP_TRY(hipMalloc(&s->g_docs, sizeof(int32_t) * W * out), "hipMalloc(shard lists)");
+    HIP_TRY(hipMalloc(&s->g_scores, sizeof(float) * W * out), "hipMalloc(shard lists)");
+    s->cap_g = W * out;
+  }
+  if (out > s->cap_m) {
+    hipFree(s->m_docs);
+    hipFree(s->m_scores);
+    s->m_docs = nullptr;
+    s->m_scores = nullptr;
+    HIP_TRY(hipMalloc(&s->m_docs, sizeof(int32_t) * out), "hipMalloc(merged)");
+    HIP_TRY(hipMalloc(&s->m_scores, sizeof(float) * out), "hipMalloc(merged)");
+    s->cap_m = out;
+  }
+  // every shard: H2D queries + search on its own stream, then an event
+  for (int64_t r = 0; r < W; ++r) {
+    bm25_index* h = s->shards[r];
+    std::lock_guard<std::mutex> lh(h->mu);
+    HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+    int rc = ensure_io(h, Q * T, out);
+    if (rc) return rc;
+    if (Q * T > 0)
+      HIP_TRY(hipMemcpyAsync(h->d_q, queries, sizeof(int32_t) * Q * T, hipMemcpyHostToDevice,
+                             h->stream), "H2D queries");
+    rc = run_search(h, h->d_q, Q, T, k, h->d_docs, h->d_scores, h->stream);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(s->done[r], h->stream), "hipEventRecord");
+  }
+  // gather on shard 0's stream (peer copies after each shard's event), merge, D2H
+  HIP_TRY(hipSetDevice(h0->ix.device), "hipSetDevice");
+  for (int64_t r = 0; r < W; ++r) {
+    bm25_index* h = s->shards[r];
+    HIP_TRY(hipStreamWaitEvent(h0->stream, s->done[r], 0), "hipStreamWaitEvent");
+    HIP_TRY(hipMemcpyPeerAsync(s->g_docs + r * out, h0->ix.device, h->d_docs, h->ix.device,
+                               sizeof(int32_t) * out, h0->stream), "peer copy");
+    HIP_TRY(hipMemcpyPeerAsync(s->g_scores + r * out, h0->ix.device, h->d_scores, h->ix.device,
+                               sizeof(float) * out, h0->stream), "peer copy");
+  }
+  HIP_TRY(launch_merge_lists(s->g_docs, s->g_scores, W, Q, k, s->m_docs, s->m_scores, h0->stream),
+          "merge_lists launch");
+  HIP_TRY(hipMemcpyAsync(out_docs, s->m_docs, sizeof(int32_t) * out, hipMemcpyDeviceToHost,
+                         h0->stream), "D2H docs");
+  HIP_TRY(hipMemcpyAsync(out_scores, s->m_scores, sizeof(float) * out, hipMemcpyDeviceToHost,
+                         h0->stream), "D2H scores");
+  HIP_TRY(hipStreamSynchronize(h0->stream), "sharded search sync");
+  return BM25_OK;
+}
+
+int bm25_sharded_info(const bm25_sharded* s, int64_t* n_shards, int64_t* shard_lo,
+                      int64_t* shard_hi) {
+  if (!s) return fail(BM25_EINVAL, "NULL index");
+  if (n_shards) *n_shards = (int64_t)s->shards.size();
+  for (size_t i = 0; i < s->shards.size(); ++i) {
+    if (shard_lo) shard_lo[i] = s->lo[i];
+    if (shard_hi) shard_hi[i] = s->hi[i];
+  }
+  return BM25_OK;
+}
+
+}  // extern "C"

@@ -13,6 +13,10 @@ Fixtures
                  bm25_test.py:23 through vocab.index.json, outputs of
                  BM25v.search, plus the two error messages
   main_demo.npz  bm25_native.py:219-248 (2x3 dense -> CSC, query [[0,1]], k=1)
+  bm25_dense.npz the reference's dense BM25 model (bm25.py:6-178) fitted on
+                 its own __main__ corpus (bm25.py:182-196): bm25_matrix, and
+                 get_scores / get_top_n(n=5) of a few queries (OOV, duplicate
+                 terms, duplicate documents -> tied scores)
   synth_small.npz  numpy-seeded 3000-doc / 400-term index; 48 queries with -1
                  padding, duplicate tokens, all-padding rows and rare-term rows
                  (zero-fill); k in {1, 10, 100}; outputs + `tied` masks computed
@@ -155,7 +159,42 @@ def synth_small():
     np.savez_compressed(os.path.join(OUT, "synth_small.npz"), **out)
 
 
+def bm25_dense():
+    import bm25 as ref_bm25  # the reference's dense model (pure numpy)
+    docs = [
+        "The quick brown fox jumps over the lazy dog",
+        "Some other text",
+        "The quick rabbit runs past the brown fox",
+        "The quick rabbit jumps over the brown dog",
+        "The quick dog chases past the lazy fox",
+        "The quick dog runs through the tall trees",
+        "The quick brown fox jumps over the lazy dog",
+        "The brown dog sleeps under the shady tree",
+        "The brown rabbit hops under the tall tree",
+        "The brown fox runs through the forest trees",
+        "The brown fox watches the sleeping rabbit",
+        "The lazy fox watches over the sleeping dog",
+        "The lazy dog watches the quick rabbit",
+    ]  # bm25.py:182-196
+    corpus = [d.lower().split() for d in docs]
+    queries = ["quick brown fox", "lazy dog", "sleeping rabbit tree", "fox fox fox",
+               "unknown words only", "the", "tall trees shady forest watches"]
+    model = ref_bm25.BM25()
+    model.fit(corpus)
+    out = {"docs": np.array(docs), "queries": np.array(queries),
+           "bm25_matrix": model.bm25_matrix, "vocabulary": np.array(model.vocabulary)}
+    for i, q in enumerate(queries):
+        toks = q.lower().split()
+        out[f"scores_{i}"] = np.asarray(model.get_scores(toks))
+        top = model.get_top_n(toks, corpus, n=5)
+        out[f"top_scores_{i}"] = np.array([t[0] for t in top], np.float64)
+        # the returned documents, as corpus indices (duplicate documents: first match)
+        out[f"top_docs_{i}"] = np.array([corpus.index(t[1]) for t in top], np.int64)
+    np.savez(os.path.join(OUT, "bm25_dense.npz"), **out)
+
+
 if __name__ == "__main__":
+    bm25_dense()
     animal()
     main_demo()
     synth_small()

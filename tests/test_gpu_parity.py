@@ -303,3 +303,63 @@ def test_kernel_variants_bit_exact(gpu, variant, monkeypatch):
         fallback += index.search_stats()["fallback_queries"]
     if "BM25_LIST_CAP" in variant:
         assert fallback > 0
+
+
+def test_sharded_index_multi_shard_one_process(gpu):
+    """bm25_sharded_*: the same GPU listed three times = three shards on their
+    own streams, peer-copied lists, HIP merge; bit-exact vs the oracle."""
+    from bm25mi import synth
+    from bm25mi.index import ShardedIndex
+    cfg = synth.Config("t", 400_000, 6000, 3_000_000, 96, 8, 100)
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    q[5, 3:] = -1
+    sh = ShardedIndex(ip, ix, dt, cfg.n_docs, devices=[0, 0, 0])
+    b = sh.shards()
+    assert len(b) == 3 and b[0][0] == 0 and b[-1][1] == cfg.n_docs
+    for k in (1, 17, 100):
+        _exact(sh.search(q, k), oracle.search_c(cfg.n_docs, ip, ix, dt, q, k))
+    with pytest.raises(ValueError, match="maximum token ID"):
+        sh.search(np.array([[cfg.n_terms]], np.int32), 3)
+    sh.close()
+
+
+def test_bm25_dense_model_golden(gpu):
+    """bm25.BM25 (drop-in of bm25.py:6-178) against the reference's own
+    outputs: get_scores within 1e-6 relative (fp32 sums of the float64 matrix's
+    values vs numpy float64 sums), get_top_n scores likewise and documents
+    exact up to the order inside groups of equal reference scores."""
+    import bm25
+    g = _load("bm25_dense.npz")
+    corpus = [d.lower().split() for d in g["docs"].tolist()]
+    m = bm25.BM25()
+    m.fit(corpus)
+    for i, q in enumerate(g["queries"].tolist()):
+        toks = q.lower().split()
+        s = m.get_scores(toks)
+        assert s.dtype == np.float64 and s.shape == (len(corpus),)
+        np.testing.assert_allclose(s, g[f"scores_{i}"], rtol=1e-6, atol=1e-6)
+        top = m.get_top_n(toks, corpus, n=5)
+        rs, rd = g[f"top_scores_{i}"], g[f"top_docs_{i}"]
+        np.testing.assert_allclose([t[0] for t in top], rs, rtol=1e-6, atol=1e-6)
+        got = [t[1] for t in top]
+        for v in np.unique(np.round(rs, 5)):
+            sel = np.nonzero(np.isclose(rs, v, rtol=0, atol=1e-5))[0]
+            want = sorted(" ".join(corpus[j]) for j in rd[sel])
+            have = sorted(" ".join(got[j]) for j in sel)
+            if len(sel) == 1 or np.sum(np.isclose(g[f"scores_{i}"], v, atol=1e-5)) == len(sel):
+                assert have == want, (q, v, have, want)
+
+
+def test_bm25s_directory_drop_in(gpu, tmp_path):
+    """BM25v.from_bm25s over a bm25s index directory (the animal fixture written
+    back to disk): the bm25_test.py:23 query returns the reference's golden."""
+    import bm25_native
+    from test_bm25s_io import write_animal
+    from bm25mi.bm25s_io import query_ids
+    g, _ = write_animal(str(tmp_path))
+    m = bm25_native.BM25v.from_bm25s(str(tmp_path))
+    q = query_ids([["fish", "purr", "like", "cat"]], m.vocab, 20)
+    docs, scores = m.search(q, top_k=2)
+    assert np.array_equal(docs, g["q1_docs"])
+    assert np.array_equal(scores.view(np.uint32), g["q1_scores"].view(np.uint32))

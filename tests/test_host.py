@@ -134,3 +134,36 @@ def test_gpu_execute_query_validates_indices():
     from gpu_bm25.common import gpu_execute_query
     with pytest.raises(ValueError, match="out of range"):
         gpu_execute_query(np.ones((3, 2), np.float32), np.array([2], np.int32), None, None)
+
+
+@pytest.mark.skipif(gpu_available(), reason="exercises the no-GPU error path")
+def test_sharded_create_without_gpu_fails_loudly():
+    from bm25mi.index import ShardedIndex
+    from bm25mi._capi import HipError
+    with pytest.raises(HipError, match="no HIP device"):
+        ShardedIndex(np.array([0, 1], np.int32), np.array([0], np.int32),
+                     np.array([1.0], np.float32), 1, devices=[0, 0])
+
+
+def test_bm25_fit_matrix_matches_reference():
+    """bm25.BM25.fit (drop-in) builds the reference's float64 matrix bit for
+    bit (golden bm25_dense.npz from bm25.py); the GPU upload that follows
+    fails loudly without a GPU."""
+    import os
+    import bm25
+    from bm25mi._capi import HipError
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "bm25_dense.npz"), allow_pickle=False)
+    corpus = [d.lower().split() for d in g["docs"].tolist()]
+    m = bm25.BM25()
+    try:
+        m.fit(corpus)
+    except HipError:
+        assert not gpu_available()
+    assert m.vocabulary == g["vocabulary"].tolist()
+    assert m.bm25_matrix.dtype == np.float64
+    assert np.array_equal(m.bm25_matrix, g["bm25_matrix"])
+    assert bm25.BM25().get_top_n(["x"], corpus, n=0) == []
+    e = bm25.BM25()
+    e.fit([])
+    assert e.get_scores(["a"]).shape == (0,)
