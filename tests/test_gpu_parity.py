@@ -347,7 +347,7 @@ def test_bm25_dense_model_golden(gpu):
             sel = np.nonzero(np.isclose(rs, v, rtol=0, atol=1e-5))[0]
             want = sorted(" ".join(corpus[j]) for j in rd[sel])
             have = sorted(" ".join(got[j]) for j in sel)
-            if len(sel) == 1 or np.sum(np.isclose(g[f"scores_{i}"], v, atol=1e-5)) == len(sel):
+            if np.sum(np.isclose(g[f"scores_{i}"], v, atol=1e-5)) == len(sel):  # tie group not cut
                 assert have == want, (q, v, have, want)
 
 
