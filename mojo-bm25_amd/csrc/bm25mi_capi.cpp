@@ -188,6 +188,19 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   HIP_TRY(launch_score(h->ix, d_queries, Q, T, k, h->ws, st), "score launch");
   if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
   HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, h->ws, d_docs, d_scores, st), "select launch");
+  if (env_int("BM25_DEBUG_LISTS", 0)) {  // dev diagnostic: candidate-list sizes
+    std::vector<int32_t> c(Q);
+    hipStreamSynchronize(st);
+    hipMemcpy(c.data(), h->ws.list_cnt, sizeof(int32_t) * Q, hipMemcpyDeviceToHost);
+    double sum = 0;
+    int32_t mx = 0;
+    for (int32_t x : c) {
+      sum += x;
+      mx = std::max(mx, x);
+    }
+    fprintf(stderr, "lists: mean %.1f max %d cap %d\n", sum / std::max<int64_t>(Q, 1), mx,
+            h->ws.list_cap);
+  }
   if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
   if (h->prof) {
     h->score_launches += 1;
@@ -305,6 +318,10 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     TRYC(hipMemcpyAsync(ix.val, data, sizeof(float) * nnz, hipMemcpyHostToDevice, h->stream), "H2D data");
   }
   TRYC(launch_build_tables(ix, d_indices, d_err, h->stream), "build_tables launch");
+  // non-negative values (no NaN): every doc's running sum only grows, which
+  // lets the REST pass flag candidates while adding (bm25mi_kernels.hip)
+  ix.nonneg = true;
+  for (int64_t p = 0; p < nnz && ix.nonneg; ++p) ix.nonneg = data[p] >= 0.0f;
   int32_t herr = 0;
   TRYC(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), "D2H err");
   TRYC(hipStreamSynchronize(h->stream), "build sync");

@@ -44,11 +44,13 @@ struct IndexArgs {
   const uint32_t* rel;
   const uint16_t* ldoc;
   const float* val;
-  int64_t V, ntiles, n_docs;
+  int64_t V, ntiles, n_docs, nnz;
+  int32_t nonneg;
 };
 
 static IndexArgs args_of(const DevIndex& ix) {
-  return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs};
+  return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs,
+                   ix.nnz, ix.nonneg ? 1 : 0};
 }
 
 // One search stage of candidate selection (see the merge kernels).
@@ -550,8 +552,10 @@ struct PostingRsrc {
 
 __device__ __forceinline__ PostingRsrc posting_rsrc(const IndexArgs& a) {
   PostingRsrc r;
-  r.ldoc = __builtin_amdgcn_make_buffer_rsrc((void*)a.ldoc, 0, -1, 0x00020000);  // 2^32-1 bytes
-  r.val = __builtin_amdgcn_make_buffer_rsrc((void*)a.val, 0, -1, 0x00020000);
+  // num_records = the arrays' exact byte sizes
+  const int np = (int)(a.nnz + kPostingPad);
+  r.ldoc = __builtin_amdgcn_make_buffer_rsrc((void*)a.ldoc, 0, (int)((uint32_t)np * 2u), 0x00020000);
+  r.val = __builtin_amdgcn_make_buffer_rsrc((void*)a.val, 0, (int)((uint32_t)np * 4u), 0x00020000);
   return r;
 }
 
@@ -559,6 +563,11 @@ __device__ __forceinline__ PostingRsrc posting_rsrc(const IndexArgs& a) {
 // row's postings read the next postings (or the zeroed pad after the last
 // one) and are masked by add_rows.  Every load is issued, so the vmcnt waits
 // stay counted.
+// (Lanes past a row's postings load the following postings and are masked
+// at the adds.  Giving them an out-of-range buffer offset instead — no fetch —
+// made the config-3 score pass slower, 5.05 vs 4.77 ms: the loads are not
+// bandwidth-bound.)
+template <int DIAG>
 __device__ __forceinline__ void issue_rows(const PostingRsrc& pr, const Rows& R, int j0,
                                            uint32_t (&ld)[kJ], float (&v)[kJ]) {
   const uint32_t lane = lane_id();
@@ -587,7 +596,7 @@ __device__ __forceinline__ int rows_done(uint32_t n) { return n == 0 ? 0 : (n <=
 // the config-3 score pass 4.7x slower: 24.8 vs 5.3 ms.)
 template <int S, int NR>
 __device__ __forceinline__ void rmw_rows(float* acc, const Rows& R, int j0, uint32_t (&ld)[kJ],
-                                         float (&v)[kJ]) {
+                                         float (&v)[kJ], float th, uint64_t& hit) {
   const uint32_t lane = lane_id();
   const uint32_t trash = (1u << S) + lane;
 #pragma unroll
@@ -605,14 +614,20 @@ __device__ __forceinline__ void rmw_rows(float* acc, const Rows& R, int j0, uint
   for (int j = 0; j < NR; ++j) {
     const bool same = j + 1 < NR && !((bm >> (j + 1)) & 1u);
     if (same) x[j + 1] = acc[ld[j + 1]];
-    acc[ld[j]] = x[j] + v[j];
+    const float y = x[j] + v[j];
+    acc[ld[j]] = y;
+    hit |= __ballot(y >= th);  // th = NaN: never
     if (j + 1 < NR && !same) x[j + 1] = acc[ld[j + 1]];
   }
 }
 
+//
+// hit collects the lanes whose new running sum reached th (the REST threshold
+// score, NaN otherwise): with non-negative values a doc's running sums only
+// grow, so an item whose hit stays 0 holds no doc with a final sum >= th.
 template <int S, int DIAG>
 __device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0, uint32_t (&ld)[kJ],
-                                         float (&v)[kJ], uint32_t n) {
+                                         float (&v)[kJ], uint32_t n, float th, uint64_t& hit) {
   if (DIAG & 1) {  // ablation: consume the loads, no adds
 #pragma unroll
     for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
@@ -620,9 +635,9 @@ __device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0, uint
   }
   const int nr = rows_done(n);
   if (nr == kJ)
-    rmw_rows<S, kJ>(acc, R, j0, ld, v);
+    rmw_rows<S, kJ>(acc, R, j0, ld, v, th, hit);
   else if (nr > 0)
-    rmw_rows<S, kJ / 2>(acc, R, j0, ld, v);
+    rmw_rows<S, kJ / 2>(acc, R, j0, ld, v, th, hit);
 }
 
 // The final sums of an item's processed rows (add_rows' ranges of the D and
@@ -649,6 +664,21 @@ __device__ __forceinline__ void read_clear(float* acc, const uint32_t (&l0)[kJ],
         acc[l1[j]] = 0.f;
       }
     }
+  }
+}
+
+// Clears the processed rows' slots (read_clear without the reads).
+__device__ __forceinline__ void clear_rows(float* acc, const uint32_t (&l0)[kJ],
+                                           const uint32_t (&l1)[kJ], uint32_t nr) {
+  const uint32_t n0 = min(nr, (uint32_t)kJ), n1 = nr > (uint32_t)kJ ? nr - kJ : 0u;
+  const int r0 = rows_done(n0), r1 = rows_done(n1);
+#pragma unroll
+  for (int j = 0; j < kJ; ++j)
+    if (r0 > 0 && (j < kJ / 2 || r0 == kJ)) acc[l0[j]] = 0.f;
+  if (r1 > 0) {
+#pragma unroll
+    for (int j = 0; j < kJ; ++j)
+      if (j < kJ / 2 || r1 == kJ) acc[l1[j]] = 0.f;
   }
 }
 
@@ -896,7 +926,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
   Rows rD = make_rows(load_desc(a, tmD, cD.tile), T, 0);
   uint32_t ltD[kJ];
   float vD[kJ];
-  issue_rows(pr, rD, 0, ltD, vD);
+  issue_rows<DIAG>(pr, rD, 0, ltD, vD);
   uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
   int32_t nitem = 0;
   BM25_STAMP(7);
@@ -908,27 +938,31 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     const uint32_t nrD = rD.nrows;
     uint32_t ltX[kJ];
     float vX[kJ];
-    if (nrD > kJ) issue_rows(pr, rD, kJ, ltX, vX);
+    if (nrD > kJ) issue_rows<DIAG>(pr, rD, kJ, ltX, vX);
     const int32_t tmA = terms_of(cA);
     const Desc dB = load_desc(a, tmB, cB.tile);
     BM25_STAMP(0);
     const Rows rC = make_rows(dC, T, 0);
     uint32_t ltC[kJ];
     float vC[kJ];
-    issue_rows(pr, rC, 0, ltC, vC);
+    issue_rows<DIAG>(pr, rC, 0, ltC, vC);
     const uint64_t thC = PH == kRest ? theta[cC.qi] : 0ull;
     BM25_STAMP(1);
     // (5) item n: adds in row order, then selection
     const int64_t tile = cD.tile;
-    add_rows<S, DIAG>(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ));
-    if (nrD > kJ) add_rows<S, DIAG>(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ));
+    // REST over a non-negative index: candidates are flagged while adding
+    const bool flagged = PH == kRest && a.nonneg && (uint32_t)(thD >> 32) > score_key(0.f);
+    const float thf = flagged ? key_score((uint32_t)(thD >> 32)) : __builtin_nanf("");
+    uint64_t hit = 0;
+    add_rows<S, DIAG>(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ), thf, hit);
+    if (nrD > kJ) add_rows<S, DIAG>(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ), thf, hit);
     if (nrD > 2 * kJ) {  // heavy item: the remaining rows, block j + kJ issued before block j's adds
       const Desc dD = load_desc(a, tmD, tile);
       Rows t = rD;
       if ((2 * kJ & 63) == 0) t = make_rows(dD, T, 2 * kJ);
       uint32_t ltY[kJ];
       float vY[kJ];
-      issue_rows(pr, t, (2 * kJ) & 63, ltY, vY);
+      issue_rows<DIAG>(pr, t, (2 * kJ) & 63, ltY, vY);
       for (uint32_t j = 2 * kJ; j < nrD; j += kJ) {
         const uint32_t jn = j + kJ;
         Rows tn = t;
@@ -936,9 +970,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
         float vZ[kJ];
         if (jn < nrD) {
           if ((jn & 63) == 0) tn = make_rows(dD, T, jn);
-          issue_rows(pr, tn, (int)(jn & 63), ltZ, vZ);
+          issue_rows<DIAG>(pr, tn, (int)(jn & 63), ltZ, vZ);
         }
-        add_rows<S, DIAG>(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ));
+        add_rows<S, DIAG>(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ), thf, hit);
         t = tn;
 #pragma unroll
         for (int i = 0; i < kJ; ++i) {
@@ -951,6 +985,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     BM25_STAMP(3);
     if (DIAG & 4) {  // ablation: no selection
       zero_acc<S>(acc);
+    } else if (flagged && hit == 0) {  // no doc of this item reaches theta
+      if (nrD <= 2 * kJ)
+        clear_rows(acc, ltD, ltX, nrD);
+      else
+        zero_acc<S>(acc);
     } else if (PH == kRest && nrD <= 2 * kJ && (uint32_t)(thD >> 32) > score_key(0.f)) {
       emit_sparse(acc, ltD, ltX, nrD, tile, S, thD, list + (int64_t)cD.qi * C,
                   list_cnt + cD.qi, C);
@@ -1378,7 +1417,7 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
 // (P = 1: one exact pass, no threshold).
 int sample_stride(int64_t ntiles, int k) {
   const char* e = getenv("BM25_SAMPLE_P");
-  const int pmax = e ? atoi(e) : 16;
+  const int pmax = e ? atoi(e) : 8;
   for (int P = 64; P >= 2; P >>= 1) {
     if (P > pmax) continue;
     const int64_t nS = (ntiles + P - 1) / P;
@@ -1465,6 +1504,7 @@ static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const S
       launch_pipe<S, PH, false, 4>(ix, q, T, sg, ws, st);
     else if (diag == 5)
       launch_pipe<S, PH, false, 5>(ix, q, T, sg, ws, st);
+
     else
       launch_pipe<S, PH, false, 32>(ix, q, T, sg, ws, st);
     return;
