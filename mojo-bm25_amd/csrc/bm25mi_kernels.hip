@@ -938,7 +938,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     const uint32_t nrD = rD.nrows;
     uint32_t ltX[kJ];
     float vX[kJ];
-    if (nrD > kJ) issue_rows<DIAG>(pr, rD, kJ, ltX, vX);
+    if (nrD > kJ) issue_rows<DIAG>(pr, rD, kJ, ltX, vX);  // (unconditional: 4.98 vs 4.77 ms)
     const int32_t tmA = terms_of(cA);
     const Desc dB = load_desc(a, tmB, cB.tile);
     BM25_STAMP(0);
