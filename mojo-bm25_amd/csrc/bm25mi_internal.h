@@ -109,7 +109,11 @@ hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores,
 
 // Tile shifts with compiled kernels.
 bool tile_shift_supported(int s);
-// Sampling stride of a search (1 = no sampling).
-int sample_stride(int64_t ntiles, int k);
+// Sampling geometry of a search: stride P (1 = no sampling) and keys per
+// sample tile m.
+struct SampleGeom {
+  int P, m;
+};
+SampleGeom sample_geom(int64_t ntiles, int k);
 
 }  // namespace bm25mi

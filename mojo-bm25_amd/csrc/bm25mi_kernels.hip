@@ -58,6 +58,7 @@ struct Stage {
   const uint64_t* cand;      // [nq][nt][kTileM] exact top-kTileM keys of the stage's tiles
   int64_t nt;                // candidate tiles per query
   int32_t P;                 // candidate tile ti is tile ti * P
+  int32_t M;                 // SAMPLE: keys per sample tile
   const uint64_t* theta;     // [nq] lower bound of the k-th key (null: none)
   const uint64_t* list;      // [nq][C] keys of the other tiles above theta (null: none)
   const int32_t* list_cnt;   // [nq]
@@ -459,11 +460,7 @@ template <int PH>
 __device__ __forceinline__ int32_t tile_of32(uint32_t ti, uint32_t P) {
   return (int32_t)(PH == kSample ? ti * P : ti);
 }
-// Keys per candidate tile of a phase's cand array: 1 (SAMPLE) or kTileM (ALL).
-template <int PH>
-constexpr int cand_per_tile() {
-  return PH == kSample ? 1 : kTileM;
-}
+
 
 // ---------------------------------------------------------------------------
 // Software-pipelined pieces of the scatter phase (score_pipe_kernel).  An
@@ -736,42 +733,46 @@ __device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ]
 // tiles than L2 holds.
 // (kClaimCH, kClaimM, kCtrStride: bm25mi_internal.h)
 
-// SAMPLE items of at most 2 kJ rows: the best key among the touched docs with
-// a positive sum (0 if none), read and cleared as in emit_sparse.  Any real
-// document's key serves theta (a lower bound of the k-th key), so ignoring the
-// untouched docs and non-positive sums is safe.
-__device__ __forceinline__ uint64_t best_sparse(float* acc, const uint32_t (&l0)[kJ],
-                                                const uint32_t (&l1)[kJ], uint32_t nr,
-                                                int64_t tile, int S) {
+// SAMPLE items of at most 2 kJ rows: the m best keys among the touched docs
+// with a positive sum (key 0 where there are fewer), read and cleared as in
+// emit_sparse, best first into out[0..m).  Any m distinct real documents'
+// keys serve theta (a lower bound of the k-th key), so ignoring the untouched
+// docs and non-positive sums is safe.  Each round takes the wave's best key
+// (smallest doc among equal keys); its lane drops it and the next round runs.
+template <int M>
+__device__ __forceinline__ void best_sparse(float* acc, const uint32_t (&l0)[kJ],
+                                            const uint32_t (&l1)[kJ], uint32_t nr, int64_t tile,
+                                            int S, uint64_t* __restrict__ out) {
   float x[2 * kJ];
   read_clear(acc, l0, l1, nr, x);
-  uint32_t bk = 0, bd = 0;
+  uint32_t key[2 * kJ];
 #pragma unroll
-  for (int j = 0; j < 2 * kJ; ++j) {
-    const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
-    const uint32_t key = x[j] > 0.f ? score_key(x[j]) : 0u;
-    bd = key > bk ? l : bd;
-    bk = key > bk ? key : bk;
+  for (int j = 0; j < 2 * kJ; ++j) key[j] = x[j] > 0.f ? score_key(x[j]) : 0u;
+  const uint32_t base = (uint32_t)(tile << S);
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    uint32_t bk = 0, bd = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < 2 * kJ; ++j) {
+      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
+      const bool better = key[j] > bk || (key[j] == bk && key[j] != 0u && l < bd);
+      bd = better ? l : bd;
+      bk = better ? key[j] : bk;
+    }
+    const uint32_t wm = wave_max_u32(bk);
+    if (wm == 0) {  // fewer than m positive docs
+      if (lane_id() == 0) out[r] = 0ull;
+      continue;
+    }
+    const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk == wm ? 0xFFFFFFFFu - bd : 0u);
+    if (lane_id() == 0) out[r] = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (base + doc));
+    if (r + 1 == M) break;
+#pragma unroll
+    for (int j = 0; j < 2 * kJ; ++j) {
+      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
+      key[j] = (bk == wm && l == doc) ? 0u : key[j];
+    }
   }
-  const uint32_t wm = wave_max_u32(bk);
-  if (wm == 0) return 0ull;
-  const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk == wm ? 0xFFFFFFFFu - bd : 0u);
-  return ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)((tile << S) + doc));
-}
-
-// Dense form: the tile's best key over every accumulator (ties: smallest
-// doc), then the accumulators are cleared.
-template <int S>
-__device__ __forceinline__ uint64_t best_dense(float* acc, int64_t tile, int64_t n_docs) {
-  const int64_t base = tile << S;
-  const int lim = (int)min<int64_t>(1 << S, n_docs - base);
-  uint32_t bk, bd;
-  lane_best<S>(acc, lim, bk, bd);
-  zero_acc<S>(acc);
-  const uint32_t wm = wave_max_u32(bk);
-  if (wm == 0) return 0ull;
-  const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk == wm ? 0xFFFFFFFFu - bd : 0u);
-  return ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc));
 }
 
 struct Cursor {  // XCD-relative item rit = (ti, qi) and its tile; end = its chunk's end
@@ -818,8 +819,8 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
     if (PH == kRest)
       emit_above<S>(fv, tile, a.n_docs, theta[qi], list + qi * C, list_cnt + qi, C);
     else
-      select_top<S>(fv, tile, a.n_docs, cand_per_tile<PH>(),
-                    cand + (qi * nt + ti) * cand_per_tile<PH>());
+      select_top<S>(fv, tile, a.n_docs, PH == kSample ? sg.M : kTileM,
+                    cand + (qi * nt + ti) * (PH == kSample ? sg.M : kTileM));
   }
 }
 
@@ -832,7 +833,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
 // and then (4) adding item n's rows (a heavy item's further rows are loaded in
 // place) and selecting / emitting its candidates.
 // ---------------------------------------------------------------------------
-template <int S, int PH, bool QMAP, int DIAG>
+template <int S, int PH, bool QMAP, int DIAG, int SM>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 4))) void score_pipe_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t nq_host,
     const int32_t* __restrict__ nq_dev, const int32_t* __restrict__ qmap,
@@ -996,9 +997,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     } else if (PH == kRest) {
       emit_rest<S>(acc, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
     } else if (PH == kSample) {
-      const uint64_t key = nrD <= 2 * kJ ? best_sparse(acc, ltD, ltX, nrD, tile, S)
-                                         : best_dense<S>(acc, tile, a.n_docs);
-      if (lane_id() == 0) cand[(int64_t)cD.qi * nt + cD.ti] = key;
+      uint64_t* out = cand + ((int64_t)cD.qi * nt + cD.ti) * SM;
+      if (nrD <= 2 * kJ)
+        best_sparse<SM>(acc, ltD, ltX, nrD, tile, S, out);
+      else
+        select_top_lds<S>(acc, tile, a.n_docs, SM, out);
     } else {
       select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + ((int64_t)cD.qi * nt + cD.ti) * kTileM);
     }
@@ -1412,18 +1415,20 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
   return hipGetLastError();
 }
 
-// Sampling stride: every P-th tile is a sample tile; P is the largest power of
-// two <= BM25_SAMPLE_P (default 16) whose sample still yields >= 2k candidates
-// (P = 1: one exact pass, no threshold).
-int sample_stride(int64_t ntiles, int k) {
+// Sampling geometry: every P-th tile is a sample tile reporting its m best
+// keys; the first (P, m) in the order P = BM25_SAMPLE_P (default 8), 4, 2
+// (powers of two), m = 1, 2, 4 whose sample yields >= 2k keys.  P = 1: no
+// threshold — the exact top-4 path over every tile (small indices).
+SampleGeom sample_geom(int64_t ntiles, int k) {
   const char* e = getenv("BM25_SAMPLE_P");
   const int pmax = e ? atoi(e) : 8;
   for (int P = 64; P >= 2; P >>= 1) {
-    if (P > pmax) continue;
+    if (P > pmax || ntiles < 2 * P) continue;
     const int64_t nS = (ntiles + P - 1) / P;
-    if (ntiles >= 2 * P && nS >= 2 * (int64_t)k) return P;
+    for (int m = 1; m <= kTileM; m <<= 1)
+      if (nS * m >= 2 * (int64_t)k) return SampleGeom{P, m};
   }
-  return 1;
+  return SampleGeom{1, 0};
 }
 
 template <int S, int PH, class K>
@@ -1459,10 +1464,20 @@ static int32_t claim_m() {
 // Diagnostic builds (BM25_ABLATE, dev only): 1 = no adds, 4 = no selection,
 // 5 = neither, 32 = s_memtime segment stamps of the REST kernel, printed to
 // stderr per launch.
-template <int S, int PH, bool QMAP, int DIAG>
+template <int S, int PH, bool QMAP, int DIAG, int SM = 1>
 static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
                         const Workspace& ws, hipStream_t st) {
-  static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH, QMAP, DIAG>);
+  if constexpr (PH == kSample && SM == 1) {  // m keys per sample tile: a build per m
+    if (sg.M == 2) {
+      launch_pipe<S, PH, QMAP, DIAG, 2>(ix, q, T, sg, ws, st);
+      return;
+    }
+    if (sg.M == kTileM) {
+      launch_pipe<S, PH, QMAP, DIAG, kTileM>(ix, q, T, sg, ws, st);
+      return;
+    }
+  }
+  static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH, QMAP, DIAG, SM>);
   hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrInts, st);
   uint64_t* stamps = nullptr;
   if (DIAG & 32) {
@@ -1471,7 +1486,7 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
     hipMemsetAsync(buf, 0, sizeof(uint64_t) * 8 * grid * kWaves, st);
     stamps = buf;
   }
-  hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG>), dim3((unsigned)grid),
+  hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG, SM>), dim3((unsigned)grid),
                      dim3(64 * kWaves), 0, st, args_of(ix), q, (int32_t)T, sg.P, sg.nq_host,
                      sg.nq_dev, sg.qmap, ws.theta, ws.cand, ws.list, ws.list_cnt, ws.list_cap,
                      ws.wctr, claim_ch(), claim_m(), stamps);
@@ -1547,8 +1562,10 @@ template <int S>
 static void score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
                     const Workspace& ws, hipStream_t st) {
   hipMemsetAsync(ws.counters, 0, 4 * sizeof(int32_t), st);
-  const int P = sample_stride(ix.ntiles, k);
-  const Stage sg = main_stage(ix, Q, P, ws);
+  const SampleGeom sgeo = sample_geom(ix.ntiles, k);
+  const int P = sgeo.P;
+  Stage sg = main_stage(ix, Q, P, ws);
+  sg.M = sgeo.m;
   if (P == 1) {
     launch_wave<S, kAll>(ix, q, T, sg, ws, st);
     return;
@@ -1556,7 +1573,8 @@ static void score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, 
   hipMemsetAsync(ws.list_cnt, 0, sizeof(int32_t) * Q, st);
   launch_wave<S, kSample>(ix, q, T, sg, ws, st);
   hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, ws.cand,
-                     (ix.ntiles + P - 1) / P, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap);
+                     (ix.ntiles + P - 1) / P * sgeo.m, (int32_t)k, ws.theta, ws.list_cnt,
+                     ws.list_cap);
   launch_wave<S, kRest>(ix, q, T, sg, ws, st);
 }
 
@@ -1588,7 +1606,7 @@ static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k,
 template <int S>
 static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
                      const Workspace& ws, int32_t* docs, float* scores, hipStream_t st) {
-  const int P = sample_stride(ix.ntiles, k);
+  const int P = sample_geom(ix.ntiles, k).P;
   select_stage<S>(ix, q, T, k, main_stage(ix, Q, P, ws), ws, docs, scores, st);
   if (P == 1) return;
   // queries whose list overflowed: exact pass over every tile (usually none;

@@ -363,3 +363,16 @@ def test_bm25s_directory_drop_in(gpu, tmp_path):
     docs, scores = m.search(q, top_k=2)
     assert np.array_equal(docs, g["q1_docs"])
     assert np.array_equal(scores.view(np.uint32), g["q1_scores"].view(np.uint32))
+
+
+def test_sample_keys_per_tile_geometries(gpu):
+    """The sampled search with m = 1, 2 and 4 keys per sample tile (the
+    geometry a doc shard of the 8-GPU config uses: few tiles, k = 100)."""
+    from bm25mi import synth
+    cfg = synth.Config("t", 600_000, 4000, 4_000_000, 48, 8, 10)
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    index = _idx(ip, ix, dt, cfg.n_docs)
+    for k in (10, 30, 70):  # 293 tiles, P = 8: m = 1, 2, 4
+        _exact(index.search(q, k), oracle.search_c(cfg.n_docs, ip, ix, dt, q, k))
+        assert index.search_stats()["fallback_queries"] == 0
