@@ -733,45 +733,96 @@ __device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ]
 // tiles than L2 holds.
 // (kClaimCH, kClaimM, kCtrStride: bm25mi_internal.h)
 
-// SAMPLE items of at most 2 kJ rows: the m best keys among the touched docs
-// with a positive sum (key 0 where there are fewer), read and cleared as in
-// emit_sparse, best first into out[0..m).  Any m distinct real documents'
-// keys serve theta (a lower bound of the k-th key), so ignoring the untouched
-// docs and non-positive sums is safe.  Each round takes the wave's best key
-// (smallest doc among equal keys); its lane drops it and the next round runs.
+// SAMPLE keys of an item: the best key of each of M equal doc slices of the
+// tile (M distinct real documents; key 0 for a slice without one).  Any M
+// distinct real documents' keys serve theta (a lower bound of the k-th key),
+// and slice maxima cost one pass instead of M extraction rounds.
+//
+// Sparse form (items of at most 2 kJ rows): the touched docs with a positive
+// sum, read and cleared as in emit_sparse.
 template <int M>
 __device__ __forceinline__ void best_sparse(float* acc, const uint32_t (&l0)[kJ],
                                             const uint32_t (&l1)[kJ], uint32_t nr, int64_t tile,
                                             int S, uint64_t* __restrict__ out) {
   float x[2 * kJ];
   read_clear(acc, l0, l1, nr, x);
-  uint32_t key[2 * kJ];
+  const int sh = S - (M == 1 ? 0 : (M == 2 ? 1 : 2));  // slice of tile-local doc l: l >> sh
+  uint32_t bk[M], bd[M];
 #pragma unroll
-  for (int j = 0; j < 2 * kJ; ++j) key[j] = x[j] > 0.f ? score_key(x[j]) : 0u;
+  for (int i = 0; i < M; ++i) {
+    bk[i] = 0;
+    bd[i] = 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int j = 0; j < 2 * kJ; ++j) {
+    const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
+    const uint32_t key = x[j] > 0.f ? score_key(x[j]) : 0u;
+    const uint32_t sl = M == 1 ? 0u : (l >> sh);
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const bool better = sl == (uint32_t)i && (key > bk[i] || (key == bk[i] && key != 0u && l < bd[i]));
+      bd[i] = better ? l : bd[i];
+      bk[i] = better ? key : bk[i];
+    }
+  }
   const uint32_t base = (uint32_t)(tile << S);
 #pragma unroll
-  for (int r = 0; r < M; ++r) {
-    uint32_t bk = 0, bd = 0xFFFFFFFFu;
+  for (int i = 0; i < M; ++i) {
+    const uint32_t wm = wave_max_u32(bk[i]);
+    uint64_t key = 0ull;
+    if (wm != 0) {
+      const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk[i] == wm ? 0xFFFFFFFFu - bd[i] : 0u);
+      key = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (base + doc));
+    }
+    if (lane_id() == 0) out[i] = key;
+  }
+}
+
+// Dense form (heavier items): every accumulator of the tile (docs past n_docs
+// excluded), then the accumulators are cleared.  Lane entries are in doc
+// order inside each lane (entry_doc), so a slice is a contiguous run of them.
+template <int S, int M>
+__device__ __forceinline__ void best_dense(float* acc, int64_t tile, int64_t n_docs,
+                                           uint64_t* __restrict__ out) {
+  constexpr int E = (1 << S) / 64;  // entries per lane
+  const float4* a4 = reinterpret_cast<const float4*>(acc);
+  const uint32_t lane = lane_id();
+  const int64_t base = tile << S;
+  const int lim = (int)min<int64_t>(1 << S, n_docs - base);
+  uint32_t bk[M], bd[M];
 #pragma unroll
-    for (int j = 0; j < 2 * kJ; ++j) {
-      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
-      const bool better = key[j] > bk || (key[j] == bk && key[j] != 0u && l < bd);
-      bd = better ? l : bd;
-      bk = better ? key[j] : bk;
-    }
-    const uint32_t wm = wave_max_u32(bk);
-    if (wm == 0) {  // fewer than m positive docs
-      if (lane_id() == 0) out[r] = 0ull;
-      continue;
-    }
-    const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk == wm ? 0xFFFFFFFFu - bd : 0u);
-    if (lane_id() == 0) out[r] = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (base + doc));
-    if (r + 1 == M) break;
+  for (int i = 0; i < M; ++i) {
+    bk[i] = 0;
+    bd[i] = 0;
+  }
+  constexpr int per = E / 4 / M;  // float4 groups per slice
 #pragma unroll
-    for (int j = 0; j < 2 * kJ; ++j) {
-      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
-      key[j] = (bk == wm && l == doc) ? 0u : key[j];
+  for (int i = 0; i < M; ++i) {
+#pragma unroll 2
+    for (int jj = 0; jj < per; ++jj) {  // not unrolled: few accumulators live at a time
+      const int j = i * per + jj;
+      const float4 f = a4[j * 64 + lane];
+      const float fe[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t key = entry_key(fe[c], 4 * j + c, lane, lim);
+        if (key > bk[i]) {
+          bk[i] = key;
+          bd[i] = entry_doc(4 * j + c, lane);
+        }
+      }
     }
+  }
+  zero_acc<S>(acc);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const uint32_t wm = wave_max_u32(bk[i]);
+    uint64_t key = 0ull;
+    if (wm != 0) {
+      const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk[i] == wm ? 0xFFFFFFFFu - bd[i] : 0u);
+      key = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc));
+    }
+    if (lane_id() == 0) out[i] = key;
   }
 }
 
@@ -1001,7 +1052,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
       if (nrD <= 2 * kJ)
         best_sparse<SM>(acc, ltD, ltX, nrD, tile, S, out);
       else
-        select_top_lds<S>(acc, tile, a.n_docs, SM, out);
+        best_dense<S, SM>(acc, tile, a.n_docs, out);
     } else {
       select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + ((int64_t)cD.qi * nt + cD.ti) * kTileM);
     }
@@ -1415,8 +1466,9 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
   return hipGetLastError();
 }
 
-// Sampling geometry: every P-th tile is a sample tile reporting its m best
-// keys; the first (P, m) in the order P = BM25_SAMPLE_P (default 8), 4, 2
+// Sampling geometry: every P-th tile is a sample tile reporting m keys (the
+// best of each of m doc slices); the first (P, m) in the order P =
+// BM25_SAMPLE_P (default 8), 4, 2
 // (powers of two), m = 1, 2, 4 whose sample yields >= 2k keys.  P = 1: no
 // threshold — the exact top-4 path over every tile (small indices).
 SampleGeom sample_geom(int64_t ntiles, int k) {
