@@ -318,10 +318,13 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     TRYC(hipMemcpyAsync(ix.val, data, sizeof(float) * nnz, hipMemcpyHostToDevice, h->stream), "H2D data");
   }
   TRYC(launch_build_tables(ix, d_indices, d_err, h->stream), "build_tables launch");
-  // non-negative values (no NaN): every doc's running sum only grows, which
-  // lets the REST pass flag candidates while adding (bm25mi_kernels.hip)
+  // values 0 or normal positive (no NaN, no denormal): every doc's running
+  // sum only grows and is 0 or >= FLT_MIN, which lets the REST pass flag
+  // candidates while adding and complete rare queries with zero-score docs
+  // (bm25mi_kernels.hip)
   ix.nonneg = true;
-  for (int64_t p = 0; p < nnz && ix.nonneg; ++p) ix.nonneg = data[p] >= 0.0f;
+  for (int64_t p = 0; p < nnz && ix.nonneg; ++p)
+    ix.nonneg = data[p] == 0.0f || data[p] >= 1.17549435e-38f;
   int32_t herr = 0;
   TRYC(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), "D2H err");
   TRYC(hipStreamSynchronize(h->stream), "build sync");

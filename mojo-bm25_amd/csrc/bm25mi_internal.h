@@ -58,7 +58,7 @@ struct DevIndex {
   int device = 0;
   int64_t n_docs = 0, n_terms = 0, nnz = 0, doc_offset = 0;
   int tile_shift = kDefaultTileShift;
-  bool nonneg = false;  // every CSC value >= 0 (running sums are monotone)
+  bool nonneg = false;  // every CSC value is 0 or >= FLT_MIN (running sums are monotone)
   int64_t ntiles = 0;
   int64_t* indptr = nullptr;
   uint32_t* rel = nullptr;

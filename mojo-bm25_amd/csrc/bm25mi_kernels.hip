@@ -1345,24 +1345,31 @@ struct SrcLists {
   }
 };
 
+// theta of a query whose sample holds fewer than k keys, on a non-negative
+// index (values 0 or normal positive, so every sum is 0 or >= FLT_MIN): every
+// doc with a positive sum (key >= (FLT_MIN, any doc)) goes to the list, and
+// merge_first completes the top-k with the smallest doc ids outside it
+// (score 0: untouched docs or zero sums).
+constexpr uint64_t kZeroFillTheta = (uint64_t)0x80800000u << 32;
+
 // theta[q] = k-th best key among the sample tiles' keys: k real documents
 // score at least this, so it is a lower bound of the final k-th key.  A query
-// with fewer than k sample keys (a sample item reports no key when none of its
-// touched docs has a positive sum) gets no threshold: theta = all ones (a NaN
-// score: no REST key passes) and its list is marked overflowed, which sends it
-// to the exact fallback stage.
+// with fewer than k sample keys (a sample reports no key for a slice without a
+// positive sum) gets kZeroFillTheta on a non-negative index; otherwise it gets
+// no threshold: theta = all ones (a NaN score: no REST key passes) and its list
+// is marked overflowed, which sends it to the exact fallback stage.
 __global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restrict__ cand,
                                                          int64_t nS, int32_t k,
                                                          uint64_t* __restrict__ theta,
                                                          int32_t* __restrict__ list_cnt,
-                                                         int32_t C) {
+                                                         int32_t C, int32_t nonneg) {
   __shared__ uint64_t keys[kMergeP];
   const int64_t q = blockIdx.x;
   topk_of(SrcFirst{cand + q * nS}, nS, k, keys);
   if (threadIdx.x == 0) {
     const uint64_t t = keys[k - 1];
-    theta[q] = t != 0ull ? t : ~0ull;
-    if (t == 0ull) list_cnt[q] = C + 1;
+    theta[q] = t != 0ull ? t : (nonneg ? kZeroFillTheta : ~0ull);
+    if (t == 0ull && !nonneg) list_cnt[q] = C + 1;
   }
 }
 
@@ -1375,6 +1382,7 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
     int32_t* __restrict__ docs, float* __restrict__ scores) {
   __shared__ uint64_t keys[kMergeP];
   __shared__ int32_t s_nflag, s_cnt;
+  __shared__ uint32_t zf_bits[2 * kMaxK / 32];
   const int64_t qi = blockIdx.x;
   if (qi >= stage_nq(sg)) return;
   const int64_t q = sg.qmap ? (int64_t)sg.qmap[qi] : qi;
@@ -1392,6 +1400,31 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
   // can reach the top-k; every list entry is above it
   topk_compact(SrcCat{c, sg.list ? sg.list + qi * sg.C : nullptr, sg.nt * kTileM},
                sg.nt * kTileM + cnt, k, sg.theta ? sg.theta[qi] : 0ull, keys, &s_cnt);
+  if (sg.theta && sg.theta[qi] == kZeroFillTheta && cnt < k) {
+    // the list holds every positive doc: complete it with the smallest doc ids
+    // outside it (all < k + cnt), score 0
+    const int span = k + cnt;
+    for (int i = threadIdx.x; i < (span + 31) / 32; i += blockDim.x) zf_bits[i] = 0u;
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+      const uint32_t d = 0xFFFFFFFFu - (uint32_t)keys[i];
+      if (d < (uint32_t)span) atomicOr(&zf_bits[d >> 5], 1u << (d & 31));
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      int filled = 0;
+      for (int b0 = 0; b0 < span && filled < k - cnt; b0 += 64) {
+        const int id = b0 + (int)threadIdx.x;
+        const bool fr = id < span && !((zf_bits[id >> 5] >> (id & 31)) & 1u);
+        const uint64_t m = __ballot(fr);
+        const int pos = filled + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (fr && pos < k - cnt) keys[cnt + pos] = make_key(0.f, (uint32_t)id);
+        filled += __popcll(m);
+      }
+    }
+    __syncthreads();
+  }
   const uint64_t theta = keys[k - 1];
   if (k > kTileM) {
     // A tile whose kTileM-th candidate beats theta may hold unreported docs
@@ -1626,7 +1659,7 @@ static void score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, 
   launch_wave<S, kSample>(ix, q, T, sg, ws, st);
   hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, ws.cand,
                      (ix.ntiles + P - 1) / P * sgeo.m, (int32_t)k, ws.theta, ws.list_cnt,
-                     ws.list_cap);
+                     ws.list_cap, ix.nonneg ? 1 : 0);
   launch_wave<S, kRest>(ix, q, T, sg, ws, st);
 }
 

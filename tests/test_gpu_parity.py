@@ -376,3 +376,24 @@ def test_sample_keys_per_tile_geometries(gpu):
     for k in (10, 30, 70):  # 293 tiles, P = 8: m = 1, 2, 4
         _exact(index.search(q, k), oracle.search_c(cfg.n_docs, ip, ix, dt, q, k))
         assert index.search_stats()["fallback_queries"] == 0
+
+
+def test_rare_queries_zero_fill_path(gpu):
+    """Queries with fewer than k positive docs in the sample (rare terms) on a
+    non-negative index: every positive doc + the smallest untouched ids —
+    no fallback pass — bit-exact vs the oracle; a signed index takes the exact
+    fallback for the same queries."""
+    rng = np.random.default_rng(17)
+    N, V = 2_000_000, 600
+    ip, ix, dt = _rand_index(rng, N, V, 40)  # every term has <= 40 postings
+    q = rng.integers(-1, V, size=(40, 5)).astype(np.int32)
+    q[0, :] = -1
+    index = _idx(ip, ix, dt, N)
+    for k in (50, 300):
+        _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+        assert index.search_stats()["fallback_queries"] == 0
+    dt2 = dt.copy()
+    dt2[::7] *= -1
+    index2 = _idx(ip, ix, dt2, N)
+    _exact(index2.search(q, 50), oracle.search_c(N, ip, ix, dt2, q, 50))
+    assert index2.search_stats()["fallback_queries"] > 0
