@@ -7,9 +7,10 @@
 A step = one search of the whole query batch (config c3: 1024 queries, k=100)
 over the 10M-doc / 200k-term / 640M-posting synthetic CSC index, inputs already
 resident in HBM.  With N GPUs the doc axis is sharded (one contiguous doc range
-per rank); every rank searches its shard, the per-shard
-[Q, k] lists are all-gathered over RCCL and merged on the GPU, so every step
-returns the same global top-k as one GPU would.  Total work is fixed as N
+per rank); every rank samples its shard, the sample keys are
+all-gathered over RCCL (one global threshold), every rank lists its keys above
+it, and the per-shard [Q, k] lists are all-gathered and merged on the GPU, so
+every step returns the same global top-k as one GPU would.  Total work is fixed as N
 grows ("scaling": "strong").
 
 Printed by rank 0: ONE JSON line with the metric, the roofline of the
@@ -88,7 +89,7 @@ def main():
     import torch
     from bm25mi import synth
     from bm25mi.index import GpuIndex
-    from bm25mi.dist import gpu_merge, sharded_topk
+    from bm25mi.dist import gpu_merge, sharded_search
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -121,10 +122,13 @@ def main():
     stream = torch.cuda.current_stream(dev)
     merge = gpu_merge(local, stream)
 
+    sdm = max(b - a for a, b in (synth.shard_bounds(cfg.n_docs, world, r) for r in range(world)))
+
     def step():
-        index.search_device(dq, k, d_docs, d_scores, stream)
-        if world > 1:  # RCCL all-gather of the [Q, k] lists + HIP merge (bm25mi.dist)
-            sharded_topk(d_docs, d_scores, merge)
+        if world > 1:  # global theta: RCCL all-gathers of sample keys and [Q, k] lists (bm25mi.dist)
+            sharded_search(index, dq, k, sdm, d_docs, d_scores, merge, stream)
+        else:
+            index.search_device(dq, k, d_docs, d_scores, stream)
 
     for _ in range(args.warmup):
         step()

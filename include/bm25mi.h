@@ -128,6 +128,36 @@ int bm25_merge_topk_device(int device, const int32_t* d_docs,
                            void* stream);
 
 /*
+ * Doc-sharded search with a GLOBAL threshold, one rank per GPU (the
+ * multi-process form of bm25_search_device).  Every rank
+ * holds one doc shard (bm25_index_create with its doc_offset) and searches
+ * the same query batch in two halves around one all-gather:
+ *   bm25_sample_width(idx, shard_docs_max, world, k, &S): keys per query each
+ *     rank samples (the same on every rank: shard_docs_max = the largest
+ *     shard's document count; S = 0: shards too small to sample);
+ *   bm25_search_sample_device(...): this shard's sample keys -> d_keys
+ *     (u64 [Q][S], zero-padded);
+ *   (caller) all-gather d_keys of every rank -> d_all_keys [world][Q][S];
+ *   bm25_search_finish_device(...): theta = the k-th best key of the world's
+ *     sample (k real documents score at least this), then every key >= theta
+ *     of this shard -> [Q, k] (global doc ids; padded with doc -1 / score bits
+ *     0xFFFFFFFF where the shard holds fewer), or the shard's exact top-k for
+ *     queries the threshold cannot serve.
+ * Merging the world's [Q, k] lists with bm25_merge_topk_device (padding
+ * sorts last) gives exactly the single-index top-k.  world = 1 is a plain
+ * search.  Replaces no reference call: the reference is single-device.
+ */
+int bm25_sample_width(const bm25_index* idx, int64_t shard_docs_max, int32_t world, int32_t k,
+                      int64_t* width);
+int bm25_search_sample_device(bm25_index* idx, const int32_t* d_queries, int64_t Q, int64_t T,
+                              int32_t k, int32_t world, int64_t shard_docs_max,
+                              uint64_t* d_keys, void* stream);
+int bm25_search_finish_device(bm25_index* idx, const int32_t* d_queries, int64_t Q, int64_t T,
+                              int32_t k, int32_t world, int64_t shard_docs_max,
+                              const uint64_t* d_all_keys, int32_t* d_docs, float* d_scores,
+                              void* stream);
+
+/*
  * Doc-sharded index over several devices of ONE process.
  * The reference is single-device (DEVICE_ID = 0, main.py:205, graph.py:95);
  * this is the build's multi-GPU form of BM25v.index / BM25v.search

@@ -64,6 +64,10 @@ _SIGS = {
     "bm25_sharded_search": ([_P, _P, _I64, _I64, _I32, _P, _P], ctypes.c_int),
     "bm25_sharded_info": ([_P, _PI64, _P, _P], ctypes.c_int),
     "bm25_sharded_destroy": ([_P], ctypes.c_int),
+    "bm25_sample_width": ([_P, _I64, _I32, _I32, _PI64], ctypes.c_int),
+    "bm25_search_sample_device": ([_P, _P, _I64, _I64, _I32, _I32, _I64, _P, _P], ctypes.c_int),
+    "bm25_search_finish_device": ([_P, _P, _I64, _I64, _I32, _I32, _I64, _P, _P, _P, _P],
+                                  ctypes.c_int),
 }
 for _name, (_args, _res) in _SIGS.items():
     _f = getattr(lib, _name)

@@ -78,3 +78,39 @@ def gpu_merge(device: int, stream=None) -> MergeFn:
         return out_d, out_s
 
     return merge
+
+
+def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
+                   d_docs: torch.Tensor, d_scores: torch.Tensor, merge: MergeFn, stream=None,
+                   group: Optional[dist.ProcessGroup] = None,
+                   exchange: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
+                   ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """One rank's doc-sharded search with a GLOBAL threshold (bm25_search_
+    sample/finish_device): this shard's sample keys are all-gathered, theta =
+    the k-th best key of the whole sample, the shard lists its keys >= theta,
+    and the lists are all-gathered and merged.  Two collectives per batch:
+    W*Q*S*8 B of sample keys (S ~ 2k/W: ~200 KB per rank at config 3) and the
+    [Q, k] lists.  ``exchange`` replaces the key all-gather (tests)."""
+    world = dist.get_world_size(group) if exchange is None else None
+    Q = d_queries.shape[0]
+    if exchange is not None:
+        world = int(exchange.world)  # type: ignore[attr-defined]
+    S = index.sample_width(k, world, shard_docs_max)
+    keys = torch.zeros((Q, max(S, 1)), dtype=torch.int64, device=d_queries.device)
+    if S > 0:
+        index.search_sample_device(d_queries, k, world, shard_docs_max, keys, stream)
+    if exchange is not None:
+        all_keys = exchange(keys)
+    elif world > 1 and S > 0:
+        all_keys = torch.empty((world,) + tuple(keys.shape), dtype=keys.dtype, device=keys.device)
+        if dist.get_backend(group) == "gloo":
+            dist.all_gather(list(all_keys.unbind(0)), keys, group=group)
+        else:
+            dist.all_gather_into_tensor(all_keys, keys, group=group)
+    else:
+        all_keys = keys.unsqueeze(0)
+    index.search_finish_device(d_queries, k, world, shard_docs_max, all_keys, d_docs, d_scores,
+                               stream)
+    if exchange is not None:
+        return d_docs, d_scores
+    return sharded_topk(d_docs, d_scores, merge, group)

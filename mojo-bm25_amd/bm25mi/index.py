@@ -111,6 +111,36 @@ class GpuIndex:
                                      int(k), ctypes.c_void_p(d_docs.data_ptr()),
                                      ctypes.c_void_p(d_scores.data_ptr()), ctypes.c_void_p(s)))
 
+    # -------------------------------------------- doc-sharded, global theta
+    def sample_width(self, k: int, world: int, shard_docs_max: int) -> int:
+        w = ctypes.c_int64()
+        check(lib.bm25_sample_width(self._h, int(shard_docs_max), int(world), int(k),
+                                    ctypes.byref(w)))
+        return w.value
+
+    def search_sample_device(self, d_queries, k: int, world: int, shard_docs_max: int, d_keys,
+                             stream=None) -> None:
+        """This shard's sample keys (torch int64/uint64 [Q, S] on the device)."""
+        Q, T = d_queries.shape
+        s = getattr(stream, "cuda_stream", stream) or 0
+        check(lib.bm25_search_sample_device(self._h, ctypes.c_void_p(d_queries.data_ptr()), Q, T,
+                                            int(k), int(world), int(shard_docs_max),
+                                            ctypes.c_void_p(d_keys.data_ptr()),
+                                            ctypes.c_void_p(s)))
+
+    def search_finish_device(self, d_queries, k: int, world: int, shard_docs_max: int,
+                             d_all_keys, d_docs, d_scores, stream=None) -> None:
+        """Global theta from every shard's sample keys ([W, Q, S]), then this
+        shard's keys >= theta as a padded [Q, k] list (global doc ids)."""
+        Q, T = d_queries.shape
+        s = getattr(stream, "cuda_stream", stream) or 0
+        check(lib.bm25_search_finish_device(self._h, ctypes.c_void_p(d_queries.data_ptr()), Q, T,
+                                            int(k), int(world), int(shard_docs_max),
+                                            ctypes.c_void_p(d_all_keys.data_ptr()),
+                                            ctypes.c_void_p(d_docs.data_ptr()),
+                                            ctypes.c_void_p(d_scores.data_ptr()),
+                                            ctypes.c_void_p(s)))
+
     def scores_dense(self, query) -> np.ndarray:
         """All n_docs fp32 scores of one query (zero for untouched docs)."""
         q = np.ascontiguousarray(np.asarray(query).ravel(), dtype=np.int32)

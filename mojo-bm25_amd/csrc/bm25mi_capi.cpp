@@ -73,6 +73,7 @@ struct bm25_index {
   double score_ms = 0.0, total_ms = 0.0;
   int64_t score_launches = 0, searches = 0, rescored = 0;
   int64_t device_bytes = 0;
+  EventPair* split_ev = nullptr;  // events of a sample/finish search in flight
 };
 
 namespace {
@@ -187,7 +188,8 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
   HIP_TRY(launch_score(h->ix, d_queries, Q, T, k, h->ws, st), "score launch");
   if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
-  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, h->ws, d_docs, d_scores, st), "select launch");
+  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, sample_geom(h->ix.ntiles, k, 1).P, h->ws,
+                        d_docs, d_scores, st), "select launch");
   if (env_int("BM25_DEBUG_LISTS", 0)) {  // dev diagnostic: candidate-list sizes
     std::vector<int32_t> c(Q);
     hipStreamSynchronize(st);
@@ -412,6 +414,71 @@ int bm25_search_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
   return run_search(h, d_queries, Q, T, k, d_docs, d_scores, (hipStream_t)stream);
+}
+
+// Two-phase search of W doc shards with a global threshold (bm25mi.h).
+static SampleGeom shard_geom(const bm25_index* h, int64_t shard_docs_max, int32_t world, int k) {
+  const int64_t D = 1ll << h->ix.tile_shift;
+  const int64_t nt = std::max<int64_t>((std::max<int64_t>(shard_docs_max, h->ix.n_docs) + D - 1) / D, 1);
+  return sample_geom(nt, k, std::max(world, 1));
+}
+
+int bm25_sample_width(const bm25_index* h, int64_t shard_docs_max, int32_t world, int32_t k,
+                      int64_t* width) {
+  if (!h || !width) return fail(BM25_EINVAL, "NULL argument");
+  if (world < 1 || k < 0) return fail(BM25_EINVAL, "bad world=%d or k=%d", world, k);
+  *width = k == 0 ? 0 : shard_geom(h, shard_docs_max, world, k).S;
+  return BM25_OK;
+}
+
+int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T,
+                              int32_t k, int32_t world, int64_t shard_docs_max, uint64_t* d_keys,
+                              void* stream) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (Q < 0 || T < 0 || world < 1) return fail(BM25_EINVAL, "bad shape");
+  int rc = check_k(h, k);
+  if (rc) return rc;
+  if (Q == 0 || k == 0) return BM25_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  rc = ensure_ws(h, Q, T, k);
+  if (rc) return rc;
+  const hipStream_t st = (hipStream_t)stream;
+  h->split_ev = next_events(h);
+  if (h->split_ev) HIP_TRY(hipEventRecord(h->split_ev->a, st), "hipEventRecord");
+  const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
+  HIP_TRY(launch_sample(h->ix, d_queries, Q, T, g, d_keys, h->ws, st), "sample launch");
+  return BM25_OK;
+}
+
+int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T,
+                              int32_t k, int32_t world, int64_t shard_docs_max,
+                              const uint64_t* d_all_keys, int32_t* d_docs, float* d_scores,
+                              void* stream) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (Q < 0 || T < 0 || world < 1) return fail(BM25_EINVAL, "bad shape");
+  int rc = check_k(h, k);
+  if (rc) return rc;
+  if (Q == 0 || k == 0) return BM25_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  rc = ensure_ws(h, Q, T, k);
+  if (rc) return rc;
+  const hipStream_t st = (hipStream_t)stream;
+  const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
+  HIP_TRY(launch_finish(h->ix, d_queries, Q, T, k, g, world, d_all_keys, h->ws, st),
+          "finish launch");
+  EventPair* ev = h->split_ev;
+  h->split_ev = nullptr;
+  if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
+  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, g.P, h->ws, d_docs, d_scores, st),
+          "select launch");
+  if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
+  if (h->prof) {
+    h->score_launches += 1;
+    h->searches += 1;
+  }
+  return BM25_OK;
 }
 
 int bm25_scores_dense(bm25_index* h, const int32_t* query, int64_t T, float* out_scores) {

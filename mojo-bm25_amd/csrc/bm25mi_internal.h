@@ -90,16 +90,35 @@ inline int64_t maxflag_for(int k, int64_t ntiles) {
   return m < ntiles ? m : (ntiles > 0 ? ntiles : 1);
 }
 
+// Sampling geometry of a search over W doc shards of ntiles tiles each:
+// stride P (1 = no sampling), m keys per sample tile, S keys per query per
+// shard.
+struct SampleGeom {
+  int P, m;
+  int64_t S;
+};
+SampleGeom sample_geom(int64_t ntiles, int k, int W);
+
 // Kernel launchers (bm25mi_kernels.hip).  All enqueue on `stream`.
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,
                                int32_t* d_err, hipStream_t stream);
-// Score pass: sample tiles -> exact top-kTileM keys, theta, other tiles ->
-// keys above theta (or every tile exact when the index is too small to sample).
+// Score pass of a single-index search: SAMPLE + theta + REST (or the exact
+// pass when the index is too small to sample).
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                         int k, const Workspace& ws, hipStream_t stream);
-// Merge + rescore + final merge, then the exact fallback stage.
+// The same in two halves for W doc shards searched together: each shard's
+// sample keys [Q][g.S] -> (all-gather across shards) -> theta over [W][Q][g.S]
+// + REST.
+hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                         const SampleGeom& g, uint64_t* keys, const Workspace& ws,
+                         hipStream_t stream);
+hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                         int k, const SampleGeom& g, int W, const uint64_t* all_keys,
+                         const Workspace& ws, hipStream_t stream);
+// Merge (+ rescore + final merge), then the exact fallback stage; P = the
+// search's sampling stride.
 hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries,
-                         int64_t Q, int64_t T, int k, const Workspace& ws,
+                         int64_t Q, int64_t T, int k, int P, const Workspace& ws,
                          int32_t* d_docs, float* d_scores, hipStream_t stream);
 hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query,
                                int64_t T, float* d_out, hipStream_t stream);
@@ -109,11 +128,5 @@ hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores,
 
 // Tile shifts with compiled kernels.
 bool tile_shift_supported(int s);
-// Sampling geometry of a search: stride P (1 = no sampling) and keys per
-// sample tile m.
-struct SampleGeom {
-  int P, m;
-};
-SampleGeom sample_geom(int64_t ntiles, int k);
 
 }  // namespace bm25mi

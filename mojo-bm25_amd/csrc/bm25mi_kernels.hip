@@ -56,6 +56,8 @@ static IndexArgs args_of(const DevIndex& ix) {
 // One search stage of candidate selection (see the merge kernels).
 struct Stage {
   const uint64_t* cand;      // [nq][nt][kTileM] exact top-kTileM keys of the stage's tiles
+  uint64_t* cand_out;        // where the score pass writes its keys (SAMPLE / ALL)
+  int64_t cstride;           // keys per query row of cand_out
   int64_t nt;                // candidate tiles per query
   int32_t P;                 // candidate tile ti is tile ti * P
   int32_t M;                 // SAMPLE: keys per sample tile
@@ -871,7 +873,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
       emit_above<S>(fv, tile, a.n_docs, theta[qi], list + qi * C, list_cnt + qi, C);
     else
       select_top<S>(fv, tile, a.n_docs, PH == kSample ? sg.M : kTileM,
-                    cand + (qi * nt + ti) * (PH == kSample ? sg.M : kTileM));
+                    sg.cand_out + qi * sg.cstride + ti * (PH == kSample ? sg.M : kTileM));
   }
 }
 
@@ -890,7 +892,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     const int32_t* __restrict__ nq_dev, const int32_t* __restrict__ qmap,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
     int32_t* __restrict__ list_cnt, int32_t C, int32_t* __restrict__ wctr, int32_t claim_ch,
-    int32_t claim_m, uint64_t* __restrict__ stamps) {
+    int32_t claim_m, int64_t cstride, uint64_t* __restrict__ stamps) {
   constexpr int D = 1 << S;
   constexpr int DP = D + 64;  // accumulators + one trash slot per lane (add_rows)
   __shared__ __attribute__((aligned(16))) float acc_all[kWaves * DP];
@@ -1048,13 +1050,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     } else if (PH == kRest) {
       emit_rest<S>(acc, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
     } else if (PH == kSample) {
-      uint64_t* out = cand + ((int64_t)cD.qi * nt + cD.ti) * SM;
+      uint64_t* out = cand + (int64_t)cD.qi * cstride + (int64_t)cD.ti * SM;
       if (nrD <= 2 * kJ)
         best_sparse<SM>(acc, ltD, ltX, nrD, tile, S, out);
       else
         best_dense<S, SM>(acc, tile, a.n_docs, out);
     } else {
-      select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + ((int64_t)cD.qi * nt + cD.ti) * kTileM);
+      select_top_lds<S>(acc, tile, a.n_docs, kTileM,
+                        cand + (int64_t)cD.qi * cstride + (int64_t)cD.ti * kTileM);
     }
     BM25_STAMP(4);
     // rotate the pipeline
@@ -1300,6 +1303,11 @@ __device__ __forceinline__ void write_result(const uint64_t* keys, int k, int64_
                                              float* __restrict__ scores) {
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     const uint64_t key = keys[i];
+    if (key == 0ull) {  // padding (a shard's list under a global theta): maps back to key 0
+      docs[row * k + i] = -1;
+      scores[row * k + i] = __uint_as_float(0xFFFFFFFFu);
+      continue;
+    }
     docs[row * k + i] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)key) + doc_offset);
     scores[row * k + i] = key_score((uint32_t)(key >> 32));
   }
@@ -1358,14 +1366,23 @@ constexpr uint64_t kZeroFillTheta = (uint64_t)0x80800000u << 32;
 // positive sum) gets kZeroFillTheta on a non-negative index; otherwise it gets
 // no threshold: theta = all ones (a NaN score: no REST key passes) and its list
 // is marked overflowed, which sends it to the exact fallback stage.
-__global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restrict__ cand,
-                                                         int64_t nS, int32_t k,
-                                                         uint64_t* __restrict__ theta,
+struct SrcShards {  // query q's sample keys of W shards: [W][Q][S]
+  const uint64_t* keys;
+  int64_t Q, S, q;
+  __device__ uint64_t operator()(int64_t i) const {
+    const int64_t w = i / S;
+    return keys[(w * Q + q) * S + (i - w * S)];
+  }
+};
+
+__global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restrict__ all_keys,
+                                                         int64_t W, int64_t Q, int64_t S,
+                                                         int32_t k, uint64_t* __restrict__ theta,
                                                          int32_t* __restrict__ list_cnt,
                                                          int32_t C, int32_t nonneg) {
   __shared__ uint64_t keys[kMergeP];
   const int64_t q = blockIdx.x;
-  topk_of(SrcFirst{cand + q * nS}, nS, k, keys);
+  topk_of(SrcShards{all_keys, Q, S, q}, W * S, k, keys);
   if (threadIdx.x == 0) {
     const uint64_t t = keys[k - 1];
     theta[q] = t != 0ull ? t : (nonneg ? kZeroFillTheta : ~0ull);
@@ -1501,19 +1518,20 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
 
 // Sampling geometry: every P-th tile is a sample tile reporting m keys (the
 // best of each of m doc slices); the first (P, m) in the order P =
-// BM25_SAMPLE_P (default 8), 4, 2
-// (powers of two), m = 1, 2, 4 whose sample yields >= 2k keys.  P = 1: no
-// threshold — the exact top-4 path over every tile (small indices).
-SampleGeom sample_geom(int64_t ntiles, int k) {
+// BM25_SAMPLE_P (default 8), 4, 2 (powers of two), m = 1, 2, 4 whose sample —
+// over the W doc shards searched together (global threshold) — yields >= 2k
+// keys.  P = 1: no threshold — the exact top-4 path over every tile (small
+// indices).  S = keys per query per shard.
+SampleGeom sample_geom(int64_t ntiles, int k, int W) {
   const char* e = getenv("BM25_SAMPLE_P");
   const int pmax = e ? atoi(e) : 8;
   for (int P = 64; P >= 2; P >>= 1) {
     if (P > pmax || ntiles < 2 * P) continue;
     const int64_t nS = (ntiles + P - 1) / P;
     for (int m = 1; m <= kTileM; m <<= 1)
-      if (nS * m >= 2 * (int64_t)k) return SampleGeom{P, m};
+      if (nS * m * W >= 2 * (int64_t)k) return SampleGeom{P, m, nS * m};
   }
-  return SampleGeom{1, 0};
+  return SampleGeom{1, 0, 0};
 }
 
 template <int S, int PH, class K>
@@ -1573,8 +1591,8 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
   }
   hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG, SM>), dim3((unsigned)grid),
                      dim3(64 * kWaves), 0, st, args_of(ix), q, (int32_t)T, sg.P, sg.nq_host,
-                     sg.nq_dev, sg.qmap, ws.theta, ws.cand, ws.list, ws.list_cnt, ws.list_cap,
-                     ws.wctr, claim_ch(), claim_m(), stamps);
+                     sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, ws.list, ws.list_cnt, ws.list_cap,
+                     ws.wctr, claim_ch(), claim_m(), sg.cstride, stamps);
   if ((DIAG & 32) && PH == kRest) {
     std::vector<uint64_t> h(8 * grid * kWaves);
     hipStreamSynchronize(st);
@@ -1611,15 +1629,19 @@ static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const S
   }
   static const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
   hipLaunchKernelGGL((score_wave_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0, st,
-                     args_of(ix), q, (int32_t)T, sg, ws.theta, ws.cand, ws.list, ws.list_cnt,
+                     args_of(ix), q, (int32_t)T, sg, ws.theta, sg.cand_out, ws.list, ws.list_cnt,
                      ws.list_cap);
 }
 
+// P > 1: the sampled search (its merge reads the list only: nt = 0);
+// P = 1: the exact path over every tile.
 static Stage main_stage(const DevIndex& ix, int64_t Q, int P, const Workspace& ws) {
   Stage sg{};
   sg.cand = ws.cand;
+  sg.cand_out = ws.cand;
+  sg.cstride = ix.ntiles * kTileM;
   sg.P = P;
-  sg.nt = P > 1 ? 0 : ix.ntiles;  // sampled search: the merge reads the list only
+  sg.nt = P > 1 ? 0 : ix.ntiles;
   sg.nq_host = (int32_t)Q;
   if (P > 1) {
     sg.theta = ws.theta;
@@ -1635,6 +1657,8 @@ static Stage main_stage(const DevIndex& ix, int64_t Q, int P, const Workspace& w
 static Stage fallback_stage(const DevIndex& ix, int64_t Q, const Workspace& ws) {
   Stage sg{};
   sg.cand = ws.cand;
+  sg.cand_out = ws.cand;
+  sg.cstride = ix.ntiles * kTileM;
   sg.P = 1;
   sg.nt = ix.ntiles;
   sg.qmap = ws.fb;
@@ -1643,35 +1667,74 @@ static Stage fallback_stage(const DevIndex& ix, int64_t Q, const Workspace& ws) 
   return sg;
 }
 
-template <int S>
-static void score_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
-                    const Workspace& ws, hipStream_t st) {
+// SAMPLE pass: each query's S keys into keys[Q][S] (zero-padded).
+template <int S_>
+static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
+                     const SampleGeom& g, uint64_t* keys, const Workspace& ws, hipStream_t st) {
+  hipMemsetAsync(keys, 0, sizeof(uint64_t) * Q * g.S, st);
+  Stage sg = main_stage(ix, Q, g.P, ws);
+  sg.M = g.m;
+  sg.cand_out = keys;
+  sg.cstride = g.S;
+  launch_wave<S_, kSample>(ix, q, T, sg, ws, st);
+}
+
+// theta from the W shards' sample keys [W][Q][S], then the REST pass (or, P =
+// 1, the exact pass over every tile).
+template <int S_>
+static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
+                     const SampleGeom& g, int W, const uint64_t* all_keys, const Workspace& ws,
+                     hipStream_t st) {
   hipMemsetAsync(ws.counters, 0, 4 * sizeof(int32_t), st);
-  const SampleGeom sgeo = sample_geom(ix.ntiles, k);
-  const int P = sgeo.P;
-  Stage sg = main_stage(ix, Q, P, ws);
-  sg.M = sgeo.m;
-  if (P == 1) {
-    launch_wave<S, kAll>(ix, q, T, sg, ws, st);
+  Stage sg = main_stage(ix, Q, g.P, ws);
+  if (g.P == 1) {
+    launch_wave<S_, kAll>(ix, q, T, sg, ws, st);
     return;
   }
   hipMemsetAsync(ws.list_cnt, 0, sizeof(int32_t) * Q, st);
-  launch_wave<S, kSample>(ix, q, T, sg, ws, st);
-  hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, ws.cand,
-                     (ix.ntiles + P - 1) / P * sgeo.m, (int32_t)k, ws.theta, ws.list_cnt,
-                     ws.list_cap, ix.nonneg ? 1 : 0);
-  launch_wave<S, kRest>(ix, q, T, sg, ws, st);
+  hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, all_keys,
+                     (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap,
+                     ix.nonneg ? 1 : 0);
+  launch_wave<S_, kRest>(ix, q, T, sg, ws, st);
+}
+
+template <int S_>
+static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k, int P,
+                     const Workspace& ws, int32_t* docs, float* scores, hipStream_t st);
+
+#define BM25_SHIFT_DISPATCH(call)                        \
+  switch (ix.tile_shift) {                               \
+    case 10: call(10); break;                            \
+    case 11: call(11); break;                            \
+    default: return hipErrorInvalidValue;                \
+  }
+
+hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                         const SampleGeom& g, uint64_t* keys, const Workspace& ws,
+                         hipStream_t stream) {
+  if (Q == 0 || ix.ntiles == 0 || g.P == 1) return hipSuccess;
+#define CALL(s) sample_s<s>(ix, d_queries, Q, T, g, keys, ws, stream)
+  BM25_SHIFT_DISPATCH(CALL)
+#undef CALL
+  return hipGetLastError();
+}
+
+hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                         int k, const SampleGeom& g, int W, const uint64_t* all_keys,
+                         const Workspace& ws, hipStream_t stream) {
+  if (Q == 0 || ix.ntiles == 0) return hipSuccess;
+#define CALL(s) finish_s<s>(ix, d_queries, Q, T, k, g, W, all_keys, ws, stream)
+  BM25_SHIFT_DISPATCH(CALL)
+#undef CALL
+  return hipGetLastError();
 }
 
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                         int k, const Workspace& ws, hipStream_t stream) {
-  if (Q == 0 || ix.ntiles == 0) return hipSuccess;
-  switch (ix.tile_shift) {
-    case 10: score_s<10>(ix, d_queries, Q, T, k, ws, stream); break;
-    case 11: score_s<11>(ix, d_queries, Q, T, k, ws, stream); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
+  const SampleGeom g = sample_geom(ix.ntiles, k, 1);
+  hipError_t e = launch_sample(ix, d_queries, Q, T, g, ws.cand, ws, stream);
+  if (e != hipSuccess) return e;
+  return launch_finish(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream);
 }
 
 template <int S>
@@ -1688,30 +1751,27 @@ static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k,
   }
 }
 
-template <int S>
-static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
+template <int S_>
+static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k, int P,
                      const Workspace& ws, int32_t* docs, float* scores, hipStream_t st) {
-  const int P = sample_geom(ix.ntiles, k).P;
-  select_stage<S>(ix, q, T, k, main_stage(ix, Q, P, ws), ws, docs, scores, st);
+  select_stage<S_>(ix, q, T, k, main_stage(ix, Q, P, ws), ws, docs, scores, st);
   if (P == 1) return;
   // queries whose list overflowed: exact pass over every tile (usually none;
   // the kernels read their count on the device and exit at once)
   hipMemsetAsync(ws.counters, 0, 2 * sizeof(int32_t), st);
   const Stage fb = fallback_stage(ix, Q, ws);
-  launch_wave<S, kAll>(ix, q, T, fb, ws, st);
-  select_stage<S>(ix, q, T, k, fb, ws, docs, scores, st);
+  launch_wave<S_, kAll>(ix, q, T, fb, ws, st);
+  select_stage<S_>(ix, q, T, k, fb, ws, docs, scores, st);
 }
 
 hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
-                         int k, const Workspace& ws, int32_t* d_docs, float* d_scores,
+                         int k, int P, const Workspace& ws, int32_t* d_docs, float* d_scores,
                          hipStream_t stream) {
   if (Q == 0 || k == 0) return hipSuccess;
   if (ix.ntiles == 0) return hipErrorInvalidValue;
-  switch (ix.tile_shift) {
-    case 10: select_s<10>(ix, d_queries, Q, T, k, ws, d_docs, d_scores, stream); break;
-    case 11: select_s<11>(ix, d_queries, Q, T, k, ws, d_docs, d_scores, stream); break;
-    default: return hipErrorInvalidValue;
-  }
+#define CALL(s) select_s<s>(ix, d_queries, Q, T, k, P, ws, d_docs, d_scores, stream)
+  BM25_SHIFT_DISPATCH(CALL)
+#undef CALL
   return hipGetLastError();
 }
 

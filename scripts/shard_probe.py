@@ -15,14 +15,28 @@ for W in [int(x) for x in (sys.argv[1:] or ["1", "2", "4", "8"])]:
     index = GpuIndex(ip, ix, dt, hi - lo, doc_offset=lo)
     d = torch.empty((Q, k), dtype=torch.int32, device="cuda"); s = torch.empty((Q, k), device="cuda")
     st = torch.cuda.current_stream()
+    from bm25mi.dist import sharded_search
+
+    class Ex:  # all-gather stand-in: every rank's sample = this shard's
+        world = W
+
+        def __call__(self, keys):
+            return keys.unsqueeze(0).expand(W, -1, -1).contiguous()
+
+    def one():
+        if W == 1:
+            index.search_device(q, k, d, s, st)
+        else:
+            sharded_search(index, q, k, hi - lo, d, s, None, st, exchange=Ex())
+
     for _ in range(3):
-        index.search_device(q, k, d, s, st)
+        one()
     torch.cuda.synchronize()
     index.profile_enable(True)
     t0 = time.perf_counter()
     n = 10
     for _ in range(n):
-        index.search_device(q, k, d, s, st)
+        one()
     torch.cuda.synchronize()
     dt_ms = (time.perf_counter() - t0) * 1e3 / n
     p = index.profile_read()

@@ -397,3 +397,51 @@ def test_rare_queries_zero_fill_path(gpu):
     index2 = _idx(ip, ix, dt2, N)
     _exact(index2.search(q, 50), oracle.search_c(N, ip, ix, dt2, q, 50))
     assert index2.search_stats()["fallback_queries"] > 0
+
+
+@pytest.mark.parametrize("W", [1, 3, 8])
+def test_global_theta_sharded_search(gpu, W):
+    """bm25_search_sample/finish_device: W doc shards on one GPU, their sample
+    keys concatenated (the all-gather of bm25mi.dist.sharded_search), theta
+    from the whole sample, per-shard padded lists merged by the HIP merge —
+    bit-exact vs the single-index oracle."""
+    import torch
+    from bm25mi import synth
+    from bm25mi.index import GpuIndex, merge_topk_device
+    from bm25mi.dist import sharded_search
+    cfg = synth.Config("t", 1_200_000, 8000, 9_000_000, 64, 8, 100)
+    full = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    q[3, 2:] = -1
+    q[7, :] = [7990, 7991, 7992, 7993, -1, -1, -1, -1]  # rare terms: fewer than k hits
+    ref = oracle.search_c(cfg.n_docs, *full, q, cfg.k)
+    dq = torch.from_numpy(q).cuda()
+    st = torch.cuda.current_stream()
+    bounds = [synth.shard_bounds(cfg.n_docs, W, r) for r in range(W)]
+    sdm = max(hi - lo for lo, hi in bounds)
+    shards = [GpuIndex(*synth.make_index(cfg, lo, hi), hi - lo, doc_offset=lo) for lo, hi in bounds]
+    # phase 1 on every shard, then the "all-gather"
+    keys = []
+    for sh in shards:
+        S = sh.sample_width(cfg.k, W, sdm)
+        kk = torch.zeros((len(q), max(S, 1)), dtype=torch.int64, device="cuda")
+        if S > 0:
+            sh.search_sample_device(dq, cfg.k, W, sdm, kk, st)
+        keys.append(kk)
+    all_keys = torch.stack(keys)
+
+    class Ex:
+        world = W
+
+        def __call__(self, _):
+            return all_keys
+
+    lists_d = torch.empty((W, len(q), cfg.k), dtype=torch.int32, device="cuda")
+    lists_s = torch.empty((W, len(q), cfg.k), dtype=torch.float32, device="cuda")
+    for r, sh in enumerate(shards):
+        sharded_search(sh, dq, cfg.k, sdm, lists_d[r], lists_s[r], None, st, exchange=Ex())
+    md = torch.empty((len(q), cfg.k), dtype=torch.int32, device="cuda")
+    ms = torch.empty((len(q), cfg.k), dtype=torch.float32, device="cuda")
+    merge_topk_device(0, lists_d, lists_s, W, len(q), cfg.k, md, ms, st)
+    torch.cuda.synchronize()
+    _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)
