@@ -84,6 +84,9 @@ def main():
                     help="CPU baseline sample size (default: 16 for c3, 64 for c2; 0 = skip)")
     ap.add_argument("--threads", type=int, default=16, help="host threads for index generation")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only for "
+                         "rehearsing several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -97,10 +100,14 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     dist = None
+    local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
