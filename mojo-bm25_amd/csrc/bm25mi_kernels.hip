@@ -35,7 +35,10 @@ namespace bm25mi {
 
 enum Phase { kAll = 0, kSample = 1, kRest = 2 };
 
-constexpr int kJ = 8;       // posting rows (64 postings each) in flight per wave
+#ifndef BM25_KJ
+#define BM25_KJ 8
+#endif
+constexpr int kJ = BM25_KJ;  // posting rows (64 postings each) in flight per wave
 constexpr int kWaves = 4;   // independent waves per score workgroup
 constexpr int kGroup = 64;  // query terms per descriptor group (one per lane)
 
