@@ -13,6 +13,8 @@ columns with numpy; scores agree to ~1e-7 relative (north_star tolerance
 1e-4) and are returned as float64 arrays like the reference's.  Documents with
 equal scores are ranked by index ascending (the reference's
 ``argsort(...)[::-1]`` order among ties is implementation-defined).
+``get_top_n`` serves n <= 4096 (kMaxK) and raises ValueError above it, where
+the reference returns every document in order.
 """
 from __future__ import annotations
 
@@ -23,6 +25,8 @@ import numpy as np
 import scipy.sparse as sp
 
 from bm25mi.index import GpuIndex
+
+MAX_TOP_K = 4096  # kMaxK of libbm25mi (bm25mi_internal.h)
 
 
 class BM25:
@@ -125,6 +129,11 @@ class BM25:
             return []
         num = min(n, self.corpus_size)
         ids = self._query_ids(query)
+        if num > MAX_TOP_K:
+            # deviation: the reference (bm25.py:172-178) argsorts every score;
+            # the engine's top-k stops at kMaxK (use get_scores for a full ranking)
+            raise ValueError(f"get_top_n: n={num} exceeds the engine's top-k limit {MAX_TOP_K}; "
+                             "rank get_scores() instead")
         q = np.full((1, max(len(ids), 1)), -1, np.int32)
         q[0, :len(ids)] = ids
         docs, scores = self._gpu.search(q, num)

@@ -3,10 +3,11 @@
 One process per GPU.  Rank r owns the contiguous document range
 ``synth.shard_bounds(N, W, r)`` as an independent index whose ``doc_offset``
 is the global id of its first document, and searches the whole (replicated)
-query batch on it.  The only exchange of the path is this one: every rank's
-[Q, k] top-k list (global doc ids + scores) is all-gathered into [W, Q, k]
-(RCCL over xGMI with the ``nccl`` backend) and merged by the same
-(score desc, doc asc) rule, so the result is exactly the single-index top-k.
+query batch on it.  The path has two exchanges, both all-gathers (RCCL over
+xGMI with the ``nccl`` backend): every rank's sample keys (global doc ids),
+from which each rank takes the same global threshold, and every rank's
+[Q, k] list of keys above it (global doc ids + scores), merged by the same
+(score desc, doc asc) rule — so the result is exactly the single-index top-k.
 
 The reference has no multi-device path (``DEVICE_ID = 0`` at
 main.py:205); this module is the build's only collective.
@@ -39,21 +40,28 @@ def shard_bounds(n_docs: int, world: int, rank: int, align: int = 2048) -> Tuple
     return b(rank), b(rank + 1)
 
 
+def _all_gather(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """[...] on every rank -> [W, ...] (rank-major).  RCCL (backend "nccl")
+    gathers device tensors in place over xGMI; gloo (CPU tests, several ranks
+    sharing one GPU) has no into-tensor form and no device all_gather, so
+    device tensors are staged through host memory there."""
+    world = dist.get_world_size(group)
+    x = x.contiguous()
+    if dist.get_backend(group) != "gloo":
+        out = torch.empty((world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x, group=group)
+        return out
+    h = x.cpu()
+    out = torch.empty((world,) + tuple(h.shape), dtype=h.dtype)
+    dist.all_gather(list(out.unbind(0)), h, group=group)
+    return out.to(x.device)
+
+
 def all_gather_lists(docs: torch.Tensor, scores: torch.Tensor,
                      group: Optional[dist.ProcessGroup] = None
                      ) -> Tuple[torch.Tensor, torch.Tensor]:
     """All ranks' [Q, k] lists -> [W, Q, k] (rank-major), on every rank."""
-    world = dist.get_world_size(group)
-    g_docs = torch.empty((world,) + tuple(docs.shape), dtype=docs.dtype, device=docs.device)
-    g_scores = torch.empty((world,) + tuple(scores.shape), dtype=scores.dtype,
-                           device=scores.device)
-    if dist.get_backend(group) == "gloo":  # no into-tensor form on gloo
-        dist.all_gather(list(g_docs.unbind(0)), docs.contiguous(), group=group)
-        dist.all_gather(list(g_scores.unbind(0)), scores.contiguous(), group=group)
-    else:
-        dist.all_gather_into_tensor(g_docs, docs.contiguous(), group=group)
-        dist.all_gather_into_tensor(g_scores, scores.contiguous(), group=group)
-    return g_docs, g_scores
+    return _all_gather(docs, group), _all_gather(scores, group)
 
 
 def sharded_topk(docs: torch.Tensor, scores: torch.Tensor, merge: MergeFn,
@@ -80,6 +88,11 @@ def gpu_merge(device: int, stream=None) -> MergeFn:
     return merge
 
 
+def gather_keys(keys: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """All ranks' [Q, S] sample keys -> [W, Q, S] (rank-major), on every rank."""
+    return _all_gather(keys, group)
+
+
 def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
                    d_docs: torch.Tensor, d_scores: torch.Tensor, merge: MergeFn, stream=None,
                    group: Optional[dist.ProcessGroup] = None,
@@ -90,27 +103,30 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
     the k-th best key of the whole sample, the shard lists its keys >= theta,
     and the lists are all-gathered and merged.  Two collectives per batch:
     W*Q*S*8 B of sample keys (S ~ 2k/W: ~200 KB per rank at config 3) and the
-    [Q, k] lists.  ``exchange`` replaces the key all-gather (tests)."""
-    world = dist.get_world_size(group) if exchange is None else None
-    Q = d_queries.shape[0]
-    if exchange is not None:
-        world = int(exchange.world)  # type: ignore[attr-defined]
-    S = index.sample_width(k, world, shard_docs_max)
-    keys = torch.zeros((Q, max(S, 1)), dtype=torch.int64, device=d_queries.device)
-    if S > 0:
-        index.search_sample_device(d_queries, k, world, shard_docs_max, keys, stream)
-    if exchange is not None:
-        all_keys = exchange(keys)
-    elif world > 1 and S > 0:
-        all_keys = torch.empty((world,) + tuple(keys.shape), dtype=keys.dtype, device=keys.device)
-        if dist.get_backend(group) == "gloo":
-            dist.all_gather(list(all_keys.unbind(0)), keys, group=group)
+    [Q, k] lists.  ``exchange`` replaces the key all-gather (tests).
+
+    Everything — kernels and collectives — is enqueued on ``stream`` (default:
+    the current stream): the collectives order against torch's current
+    stream, so the body runs with ``stream`` made current."""
+    if stream is None:
+        stream = torch.cuda.current_stream(d_queries.device)
+    with torch.cuda.stream(stream):
+        world = dist.get_world_size(group) if exchange is None else None
+        Q = d_queries.shape[0]
+        if exchange is not None:
+            world = int(exchange.world)  # type: ignore[attr-defined]
+        S = index.sample_width(k, world, shard_docs_max)
+        keys = torch.zeros((Q, max(S, 1)), dtype=torch.int64, device=d_queries.device)
+        if S > 0:
+            index.search_sample_device(d_queries, k, world, shard_docs_max, keys, stream)
+        if exchange is not None:
+            all_keys = exchange(keys)
+        elif world > 1 and S > 0:
+            all_keys = gather_keys(keys, group)
         else:
-            dist.all_gather_into_tensor(all_keys, keys, group=group)
-    else:
-        all_keys = keys.unsqueeze(0)
-    index.search_finish_device(d_queries, k, world, shard_docs_max, all_keys, d_docs, d_scores,
-                               stream)
-    if exchange is not None:
-        return d_docs, d_scores
-    return sharded_topk(d_docs, d_scores, merge, group)
+            all_keys = keys.unsqueeze(0)
+        index.search_finish_device(d_queries, k, world, shard_docs_max, all_keys, d_docs,
+                                   d_scores, stream)
+        if exchange is not None:
+            return d_docs, d_scores
+        return sharded_topk(d_docs, d_scores, merge, group)

@@ -74,6 +74,8 @@ struct bm25_index {
   int64_t score_launches = 0, searches = 0, rescored = 0;
   int64_t device_bytes = 0;
   EventPair* split_ev = nullptr;  // events of a sample/finish search in flight
+  hipEvent_t ws_done = nullptr;    // end of the last search that used the workspace
+  hipStream_t ws_stream = nullptr; // its stream
 };
 
 namespace {
@@ -178,12 +180,28 @@ EventPair* next_events(bm25_index* h) {
   return &h->ev_pool[h->ev_used++];
 }
 
+// The workspace is shared by every search on the handle: a search enqueued
+// on another stream than the previous one first waits for that search's end
+// (ws_done, recorded after every search).
+hipError_t order_ws(bm25_index* h, hipStream_t st) {
+  if (!h->ws_done) {
+    const hipError_t e = hipEventCreateWithFlags(&h->ws_done, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    h->ws_stream = st;
+    return hipSuccess;
+  }
+  if (st == h->ws_stream) return hipSuccess;
+  h->ws_stream = st;
+  return hipStreamWaitEvent(st, h->ws_done, 0);
+}
+
 // Device pipeline on stream st; caller holds h->mu and has set the device.
 int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, int k,
                int32_t* d_docs, float* d_scores, hipStream_t st) {
   if (Q == 0 || k == 0) return BM25_OK;
   int rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
+  HIP_TRY(order_ws(h, st), "workspace order");
   EventPair* ev = next_events(h);
   if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
   HIP_TRY(launch_score(h->ix, d_queries, Q, T, k, h->ws, st), "score launch");
@@ -204,6 +222,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
             h->ws.list_cap);
   }
   if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
+  HIP_TRY(hipEventRecord(h->ws_done, st), "hipEventRecord");
   if (h->prof) {
     h->score_launches += 1;
     h->searches += 1;
@@ -219,9 +238,13 @@ void read_counters(bm25_index* h, int32_t (&cnt)[4]) {
   hipMemcpy(cnt, h->ws.counters, sizeof cnt, hipMemcpyDeviceToHost);
 }
 
-int check_k(const bm25_index* h, int64_t k) {
+// shard = true: the index is one doc shard of a larger collection, whose
+// [Q, k] lists are padded (doc -1, score bits ~0) where it holds fewer than k
+// documents; otherwise k > n_docs is numpy's argpartition error (the
+// reference's behaviour, bm25_native.py:205).
+int check_k(const bm25_index* h, int64_t k, bool shard = false) {
   if (k < 0) return fail(BM25_EINVAL, "negative dimensions are not allowed (top_k=%lld)", (long long)k);
-  if (k > h->ix.n_docs)
+  if (!shard && k > h->ix.n_docs)
     return fail(BM25_EINVAL, "kth(=%lld) out of bounds (%lld)", (long long)(h->ix.n_docs - k),
                 (long long)h->ix.n_docs);
   if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%lld exceeds the engine limit %d", (long long)k, kMaxK);
@@ -348,6 +371,7 @@ int bm25_index_destroy(bm25_index* h) {
     hipEventDestroy(p.b);
     hipEventDestroy(p.c);
   }
+  if (h->ws_done) hipEventDestroy(h->ws_done);
   free_ws(h->ws);
   hipFree(h->d_q);
   hipFree(h->d_docs);
@@ -436,7 +460,7 @@ int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q
                               void* stream) {
   if (!h) return fail(BM25_EINVAL, "NULL index");
   if (Q < 0 || T < 0 || world < 1) return fail(BM25_EINVAL, "bad shape");
-  int rc = check_k(h, k);
+  int rc = check_k(h, k, true);
   if (rc) return rc;
   if (Q == 0 || k == 0) return BM25_OK;
   std::lock_guard<std::mutex> lk(h->mu);
@@ -444,6 +468,7 @@ int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   const hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(order_ws(h, st), "workspace order");
   h->split_ev = next_events(h);
   if (h->split_ev) HIP_TRY(hipEventRecord(h->split_ev->a, st), "hipEventRecord");
   const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
@@ -457,7 +482,7 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
                               void* stream) {
   if (!h) return fail(BM25_EINVAL, "NULL index");
   if (Q < 0 || T < 0 || world < 1) return fail(BM25_EINVAL, "bad shape");
-  int rc = check_k(h, k);
+  int rc = check_k(h, k, true);
   if (rc) return rc;
   if (Q == 0 || k == 0) return BM25_OK;
   std::lock_guard<std::mutex> lk(h->mu);
@@ -465,6 +490,7 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   const hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(order_ws(h, st), "workspace order");
   const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
   HIP_TRY(launch_finish(h->ix, d_queries, Q, T, k, g, world, d_all_keys, h->ws, st),
           "finish launch");
@@ -474,6 +500,7 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, g.P, h->ws, d_docs, d_scores, st),
           "select launch");
   if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
+  HIP_TRY(hipEventRecord(h->ws_done, st), "hipEventRecord");
   if (h->prof) {
     h->score_launches += 1;
     h->searches += 1;
@@ -702,10 +729,6 @@ int bm25_sharded_search(bm25_sharded* s, const int32_t* queries, int64_t Q, int6
                 "the index.",
                 (long long)mx);
   const int64_t W = (int64_t)s->shards.size();
-  for (int64_t r = 0; r < W; ++r)
-    if (s->hi[r] - s->lo[r] < k)
-      return fail(BM25_EINVAL, "top_k=%d exceeds the %lld documents of shard %lld", k,
-                  (long long)(s->hi[r] - s->lo[r]), (long long)r);
   std::lock_guard<std::mutex> lk(s->mu);
   bm25_index* h0 = s->shards[0];
   const int64_t out = Q * (int64_t)k;

@@ -52,6 +52,10 @@ constexpr int kDefaultTileShift = 11;
 constexpr int kClaimCH = 8;
 constexpr int kClaimM = 8;  // counters allocated per XCD (4 used by default)
 constexpr int kCtrStride = 64;
+// Item order of the pipelined score kernel: bands of kBand consecutive tiles,
+// query by query inside a band; sample tiles in groups of kSampleGroup.
+constexpr int kBand = 8;
+constexpr int kSampleGroup = 8;
 constexpr int kWctrInts = 8 * kClaimM * kCtrStride;
 
 struct DevIndex {
@@ -92,10 +96,11 @@ inline int64_t maxflag_for(int k, int64_t ntiles) {
 
 // Sampling geometry of a search over W doc shards of ntiles tiles each:
 // stride P (1 = no sampling), m keys per sample tile, S keys per query per
-// shard.
+// shard, sample tiles in groups of G consecutive tiles (one group per G*P).
 struct SampleGeom {
   int P, m;
   int64_t S;
+  int G;  // sample tiles come in groups of G consecutive tiles (bm25mi_kernels.hip)
 };
 SampleGeom sample_geom(int64_t ntiles, int k, int W);
 

@@ -48,12 +48,25 @@ struct IndexArgs {
   const uint16_t* ldoc;
   const float* val;
   int64_t V, ntiles, n_docs, nnz;
+  int64_t doc_offset;  // global id of the index's first doc (sample keys are global)
   int32_t nonneg;
 };
 
 static IndexArgs args_of(const DevIndex& ix) {
   return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs,
-                   ix.nnz, ix.nonneg ? 1 : 0};
+                   ix.nnz, ix.doc_offset, ix.nonneg ? 1 : 0};
+}
+
+// Sample tiles: groups of G consecutive tiles, one group in every G*P tiles
+// (tile of sample index si, and the number of sample tiles of an index).
+// Consecutive sample tiles of a query then share the boundary cache lines of
+// its terms' posting segments, as the REST tiles do.
+__host__ __device__ inline int64_t sample_tile(int64_t si, int64_t P, int64_t G) {
+  return (si / G) * G * P + si % G;
+}
+__host__ __device__ inline int64_t sample_count(int64_t ntiles, int64_t P, int64_t G) {
+  const int64_t r = ntiles % (G * P);
+  return (ntiles / (G * P)) * G + (r < G ? r : G);
 }
 
 // One search stage of candidate selection (see the merge kernels).
@@ -62,7 +75,8 @@ struct Stage {
   uint64_t* cand_out;        // where the score pass writes its keys (SAMPLE / ALL)
   int64_t cstride;           // keys per query row of cand_out
   int64_t nt;                // candidate tiles per query
-  int32_t P;                 // candidate tile ti is tile ti * P
+  int32_t P;                 // SAMPLE: sampling stride (sample_tile)
+  int32_t G;                 // SAMPLE: sample tiles per group (sample_tile)
   int32_t M;                 // SAMPLE: keys per sample tile
   const uint64_t* theta;     // [nq] lower bound of the k-th key (null: none)
   const uint64_t* list;      // [nq][C] keys of the other tiles above theta (null: none)
@@ -252,7 +266,8 @@ __device__ __forceinline__ void take_entries(float* acc, float (&fv)[(1 << S) / 
 // ---------------------------------------------------------------------------
 template <int S>
 __device__ __forceinline__ void select_top(const float (&fv)[(1 << S) / 64], int64_t tile,
-                                           int64_t n_docs, int m, uint64_t* __restrict__ out) {
+                                           int64_t n_docs, int m, uint32_t idoff,
+                                           uint64_t* __restrict__ out) {
   constexpr int E = (1 << S) / 64;
   const uint32_t lane = lane_id();
   const int64_t base = tile << S;
@@ -275,7 +290,7 @@ __device__ __forceinline__ void select_top(const float (&fv)[(1 << S) / 64], int
     }
     const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(lmax == wm ? 0xFFFFFFFFu - ldoc : 0u);
     if (lane == ((doc >> 2) & 63u)) {
-      out[r] = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc));
+      out[r] = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc) - idoff);
       const int eb = (int)(((doc >> 8) << 2) | (doc & 3u));
       lmax = 0;
 #pragma unroll
@@ -456,14 +471,15 @@ __device__ __forceinline__ void emit_rest(float* acc, int64_t tile, int64_t n_do
   }
 }
 
-// Tiles of a phase: SAMPLE visits every P-th tile, ALL and REST every tile.
+// Tiles of a phase: SAMPLE visits the sample tiles (sample_tile), ALL and
+// REST every tile.
 template <int PH>
-__device__ __forceinline__ int64_t tile_of(int64_t ti, int P) {
-  return PH == kSample ? ti * P : ti;
+__device__ __forceinline__ int64_t tile_of(int64_t ti, int P, int G) {
+  return PH == kSample ? sample_tile(ti, P, G) : ti;
 }
 template <int PH>
-__device__ __forceinline__ int32_t tile_of32(uint32_t ti, uint32_t P) {
-  return (int32_t)(PH == kSample ? ti * P : ti);
+__device__ __forceinline__ int32_t tile_of32(uint32_t ti, uint32_t P, uint32_t G) {
+  return (int32_t)(PH == kSample ? (ti / G) * G * P + ti % G : ti);
 }
 
 
@@ -506,6 +522,9 @@ __device__ __forceinline__ uint32_t scan16(uint32_t x) {
 // An item's posting rows: each query term's segment is cut into rows of 64
 // postings (one per lane), so a row belongs to one term and needs no term
 // mask.  Lane j of the table describes row j0 + j of the item.
+// (Rows aligned to 64-posting boundaries touch 3 cache lines instead of ~5 —
+// 271 M vs 307 M L1->L2 requests per config-3 REST pass — but add ~8 % rows
+// and more items past kJ rows: 5.64 vs 4.91 ms.)
 struct Rows {
   int64_t base;    // posting index of the row's first posting (0 past the end)
   uint32_t cnt;    // postings in the row (0: past the item's rows)
@@ -563,12 +582,10 @@ __device__ __forceinline__ PostingRsrc posting_rsrc(const IndexArgs& a) {
 
 // Loads of table rows [j0, j0 + kJ): slot + score per lane.  Lanes past a
 // row's postings read the next postings (or the zeroed pad after the last
-// one) and are masked by add_rows.  Every load is issued, so the vmcnt waits
-// stay counted.
-// (Lanes past a row's postings load the following postings and are masked
-// at the adds.  Giving them an out-of-range buffer offset instead — no fetch —
-// made the config-3 score pass slower, 5.05 vs 4.77 ms: the loads are not
-// bandwidth-bound.)
+// one) and are masked by add_rows.  Every load is issued, so
+// the vmcnt waits stay counted.
+// (Giving the masked lanes an out-of-range buffer offset instead — no fetch —
+// made the config-3 score pass slower, 5.05 vs 4.77 ms, round 1.)
 template <int DIAG>
 __device__ __forceinline__ void issue_rows(const PostingRsrc& pr, const Rows& R, int j0,
                                            uint32_t (&ld)[kJ], float (&v)[kJ]) {
@@ -691,7 +708,7 @@ __device__ __forceinline__ void clear_rows(float* acc, const uint32_t (&l0)[kJ],
 // score is > 0: untouched docs (sum 0) and cleared re-reads can never pass,
 // and every touched doc is read after its last add.  The same reads return
 // the accumulator to all zeros for the next item.  Slots are add_rows'
-// (lanes past a row's postings hold their trash slot, which reads 0).
+// (masked lanes hold their trash slot, which reads 0).
 __device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ],
                                             const uint32_t (&l1)[kJ], uint32_t nr, int64_t tile,
                                             int S, uint64_t theta, uint64_t* __restrict__ list,
@@ -748,7 +765,7 @@ __device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ]
 template <int M>
 __device__ __forceinline__ void best_sparse(float* acc, const uint32_t (&l0)[kJ],
                                             const uint32_t (&l1)[kJ], uint32_t nr, int64_t tile,
-                                            int S, uint64_t* __restrict__ out) {
+                                            int S, uint32_t idoff, uint64_t* __restrict__ out) {
   float x[2 * kJ];
   read_clear(acc, l0, l1, nr, x);
   const int sh = S - (M == 1 ? 0 : (M == 2 ? 1 : 2));  // slice of tile-local doc l: l >> sh
@@ -770,7 +787,7 @@ __device__ __forceinline__ void best_sparse(float* acc, const uint32_t (&l0)[kJ]
       bk[i] = better ? key : bk[i];
     }
   }
-  const uint32_t base = (uint32_t)(tile << S);
+  const uint32_t base = (uint32_t)(tile << S) + idoff;  // global doc ids (theta_kernel)
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     const uint32_t wm = wave_max_u32(bk[i]);
@@ -788,7 +805,7 @@ __device__ __forceinline__ void best_sparse(float* acc, const uint32_t (&l0)[kJ]
 // order inside each lane (entry_doc), so a slice is a contiguous run of them.
 template <int S, int M>
 __device__ __forceinline__ void best_dense(float* acc, int64_t tile, int64_t n_docs,
-                                           uint64_t* __restrict__ out) {
+                                           uint32_t idoff, uint64_t* __restrict__ out) {
   constexpr int E = (1 << S) / 64;  // entries per lane
   const float4* a4 = reinterpret_cast<const float4*>(acc);
   const uint32_t lane = lane_id();
@@ -825,14 +842,17 @@ __device__ __forceinline__ void best_dense(float* acc, int64_t tile, int64_t n_d
     uint64_t key = 0ull;
     if (wm != 0) {
       const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk[i] == wm ? 0xFFFFFFFFu - bd[i] : 0u);
-      key = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc));
+      key = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + doc) - idoff);
     }
     if (lane_id() == 0) out[i] = key;
   }
 }
 
-struct Cursor {  // XCD-relative item rit = (ti, qi) and its tile; end = its chunk's end
-  int32_t rit, end, ti, qi, tile;
+// Item of the pipelined kernel: XCD-relative ordinal rit (end = its chunk's
+// end), phase tile ti = the tib-th tile of a band of bw tiles, query qi, and
+// the tile it scores.
+struct Cursor {
+  int32_t rit, end, ti, qi, tile, tib, bw;
 };
 
 // ---------------------------------------------------------------------------
@@ -854,7 +874,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
   float* acc = acc_all + wave * D;
   const int64_t nq = sg.nq_dev ? (int64_t)*sg.nq_dev : (int64_t)sg.nq_host;
   const int P = sg.P;
-  const int64_t nt = PH == kSample ? (a.ntiles + P - 1) / P : a.ntiles;
+  const int64_t nt = PH == kSample ? sample_count(a.ntiles, P, sg.G) : a.ntiles;
   const int64_t nitems = nt * nq;
   const int64_t per = (nitems + 7) >> 3;
   const int64_t grp = blockIdx.x & 7;
@@ -868,7 +888,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
     const int64_t ti = it / nq;
     const int64_t qi = it - ti * nq;
     const int64_t q = sg.qmap ? (int64_t)sg.qmap[qi] : qi;
-    const int64_t tile = tile_of<PH>(ti, P);
+    const int64_t tile = tile_of<PH>(ti, P, sg.G);
     add_item<S>(a, tile, queries + q * T, T, acc);
     float fv[D / 64];
     take_entries<S>(acc, fv);
@@ -876,13 +896,22 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
       emit_above<S>(fv, tile, a.n_docs, theta[qi], list + qi * C, list_cnt + qi, C);
     else
       select_top<S>(fv, tile, a.n_docs, PH == kSample ? sg.M : kTileM,
+                    PH == kSample ? (uint32_t)a.doc_offset : 0u,
                     sg.cand_out + qi * sg.cstride + ti * (PH == kSample ? sg.M : kTileM));
   }
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined persistent score kernel (1 <= T <= 64): same items, same order,
-// same per-document add order as score_wave_kernel, with iteration n issuing
+// Pipelined persistent score kernel (1 <= T <= 64): same items and the same
+// per-document add order as score_wave_kernel.  Item order: band-major — the
+// phase's tiles are cut into bands of `band` consecutive tiles, and inside a
+// band the items run query by query, each query over the band's tiles — so a
+// claimed chunk is one query over consecutive tiles: its terms' segments of
+// neighbouring tiles share cache lines (a light term has a few postings per
+// tile), and the XCD's waves read the same band of every popular term.
+// (Tile-major order, all queries of a tile back to back, re-fetched each
+// light term's lines from beyond L2 for every tile: 17 GB per config-3 REST
+// launch against 1.9 GB of batch-distinct postings.)  Iteration n issues
 //   (1) the query terms of item n+3,
 //   (2) the (indptr, rel) segment bounds of item n+2,
 //   (3) item n's second block of kJ posting rows and item n+1's first block,
@@ -895,7 +924,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     const int32_t* __restrict__ nq_dev, const int32_t* __restrict__ qmap,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
     int32_t* __restrict__ list_cnt, int32_t C, int32_t* __restrict__ wctr, int32_t claim_ch,
-    int32_t claim_m, int64_t cstride, uint64_t* __restrict__ stamps) {
+    int32_t claim_m, int64_t cstride, int32_t G, int32_t band, uint64_t* __restrict__ stamps) {
   constexpr int D = 1 << S;
   constexpr int DP = D + 64;  // accumulators + one trash slot per lane (add_rows)
   __shared__ __attribute__((aligned(16))) float acc_all[kWaves * DP];
@@ -914,7 +943,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
   }
   BM25_STAMP(7);
   const int32_t nq = QMAP ? *nq_dev : nq_host;
-  const int32_t nt = PH == kSample ? (int32_t)((a.ntiles + P - 1) / P) : (int32_t)a.ntiles;
+  const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
   const int64_t nitems = (int64_t)nt * nq;
   const int64_t per = (nitems + 7) >> 3;
   const int grp = (int)(blockIdx.x & 7);
@@ -937,15 +966,24 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
   // cursor of the next item after c: the next one of c's chunk, else the
   // first of the pending chunk; past the end it stays on c's item with
   // rit = ngi, so every stage keeps loading valid addresses
+  const int32_t nfb = nt / band;  // full bands
+  const uint32_t full_items = (uint32_t)nfb * (uint32_t)band * (uint32_t)nq;
   auto next = [&](Cursor c) -> Cursor {
     if (c.rit >= ngi) return c;
     if (c.rit + 1 < c.end) {
       ++c.rit;
-      if (++c.qi == nq) {
-        c.qi = 0;
+      if (++c.tib == c.bw) {  // the query's last tile of the band
+        c.tib = 0;
+        c.ti -= c.bw - 1;
+        if (++c.qi == nq) {  // next band
+          c.qi = 0;
+          c.ti += c.bw;
+          c.bw = min(band, nt - c.ti);
+        }
+      } else {
         ++c.ti;
       }
-      c.tile = tile_of32<PH>((uint32_t)c.ti, (uint32_t)P);
+      c.tile = tile_of32<PH>((uint32_t)c.ti, (uint32_t)P, (uint32_t)G);
       return c;
     }
     const int64_t b = ((int64_t)uniform(pending) * claim_m + cm) * claim_ch;
@@ -958,9 +996,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     n.rit = (int32_t)b;
     n.end = (int32_t)min<int64_t>(ngi, b + claim_ch);
     const uint32_t it = lo + (uint32_t)b;
-    n.ti = (int32_t)(it / (uint32_t)nq);
-    n.qi = (int32_t)(it - (uint32_t)n.ti * (uint32_t)nq);
-    n.tile = tile_of32<PH>((uint32_t)n.ti, (uint32_t)P);
+    uint32_t bb, r, bw;
+    if (it < full_items) {
+      bb = it / ((uint32_t)band * (uint32_t)nq);
+      r = it - bb * (uint32_t)band * (uint32_t)nq;
+      bw = (uint32_t)band;
+    } else {  // the last, partial band
+      bb = (uint32_t)nfb;
+      r = it - full_items;
+      bw = (uint32_t)(nt - nfb * band);
+    }
+    n.qi = (int32_t)(r / bw);
+    n.tib = (int32_t)(r - (uint32_t)n.qi * bw);
+    n.bw = (int32_t)bw;
+    n.ti = (int32_t)(bb * (uint32_t)band) + n.tib;
+    n.tile = tile_of32<PH>((uint32_t)n.ti, (uint32_t)P, (uint32_t)G);
     return n;
   };
   auto terms_of = [&](const Cursor& c) -> int32_t {
@@ -971,7 +1021,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
   Cursor c0;  // a chunk "before" the first one: next() takes the pending claim
   c0.rit = -1;
   c0.end = 0;
-  c0.ti = c0.qi = c0.tile = 0;
+  c0.ti = c0.qi = c0.tile = c0.tib = 0;
+  c0.bw = 1;
   Cursor cD = next(c0);
   if (cD.rit >= ngi) return;
   zero_acc<S>(acc);
@@ -1055,9 +1106,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     } else if (PH == kSample) {
       uint64_t* out = cand + (int64_t)cD.qi * cstride + (int64_t)cD.ti * SM;
       if (nrD <= 2 * kJ)
-        best_sparse<SM>(acc, ltD, ltX, nrD, tile, S, out);
+        best_sparse<SM>(acc, ltD, ltX, nrD, tile, S, (uint32_t)a.doc_offset, out);
       else
-        best_dense<S, SM>(acc, tile, a.n_docs, out);
+        best_dense<S, SM>(acc, tile, a.n_docs, (uint32_t)a.doc_offset, out);
     } else {
       select_top_lds<S>(acc, tile, a.n_docs, kTileM,
                         cand + (int64_t)cD.qi * cstride + (int64_t)cD.ti * kTileM);
@@ -1134,7 +1185,7 @@ __global__ __launch_bounds__(kRescoreNT) void rescore_kernel(IndexArgs a,
     const int32_t code = ws.queue[it];
     const int64_t qi = code / maxflag;
     const int64_t q = sg.qmap ? (int64_t)sg.qmap[qi] : qi;
-    const int64_t tile = (int64_t)ws.flag_tiles[code] * sg.P;
+    const int64_t tile = sample_tile(ws.flag_tiles[code], sg.P, sg.G);
     if (threadIdx.x < 64) {
       zero_acc<S>(acc);
       add_item<S>(a, tile, queries + q * T, T, acc);
@@ -1378,16 +1429,30 @@ struct SrcShards {  // query q's sample keys of W shards: [W][Q][S]
   }
 };
 
+//
+// Sample keys carry GLOBAL doc ids (doc_offset + local), so the k-th key is
+// the same on every shard; theta is then moved into this shard's frame: same
+// score, tie doc L = global - doc_offset (docs <= L of that score pass),
+// clamped to n_docs; L < 0 (the tie doc lies in an earlier shard) becomes
+// "strictly higher scores only" = (score key + 1, any doc).
 __global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restrict__ all_keys,
                                                          int64_t W, int64_t Q, int64_t S,
                                                          int32_t k, uint64_t* __restrict__ theta,
                                                          int32_t* __restrict__ list_cnt,
-                                                         int32_t C, int32_t nonneg) {
+                                                         int32_t C, int32_t nonneg,
+                                                         int64_t doc_offset, int64_t n_docs) {
   __shared__ uint64_t keys[kMergeP];
   const int64_t q = blockIdx.x;
   topk_of(SrcShards{all_keys, Q, S, q}, W * S, k, keys);
   if (threadIdx.x == 0) {
-    const uint64_t t = keys[k - 1];
+    uint64_t t = keys[k - 1];
+    if (t != 0ull) {
+      const int64_t L = (int64_t)(0xFFFFFFFFu - (uint32_t)t) - doc_offset;
+      if (L < 0)
+        t = (t | 0xFFFFFFFFull) + 1ull;
+      else
+        t = (t & ~0xFFFFFFFFull) | (uint64_t)(0xFFFFFFFFu - (uint32_t)min(L, n_docs));
+    }
     theta[q] = t != 0ull ? t : (nonneg ? kZeroFillTheta : ~0ull);
     if (t == 0ull && !nonneg) list_cnt[q] = C + 1;
   }
@@ -1398,7 +1463,7 @@ __device__ __forceinline__ int64_t stage_nq(const Stage& sg) {
 }
 
 __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
-    Stage sg, int32_t k, int64_t maxflag, int64_t doc_offset, Workspace ws,
+    Stage sg, int32_t k, int64_t maxflag, int64_t doc_offset, int64_t n_docs, Workspace ws,
     int32_t* __restrict__ docs, float* __restrict__ scores) {
   __shared__ uint64_t keys[kMergeP];
   __shared__ int32_t s_nflag, s_cnt;
@@ -1422,7 +1487,8 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
                sg.nt * kTileM + cnt, k, sg.theta ? sg.theta[qi] : 0ull, keys, &s_cnt);
   if (sg.theta && sg.theta[qi] == kZeroFillTheta && cnt < k) {
     // the list holds every positive doc: complete it with the smallest doc ids
-    // outside it (all < k + cnt), score 0
+    // outside it (all < k + cnt), score 0; a shard holding fewer than k docs
+    // leaves the rest as padding (key 0)
     const int span = k + cnt;
     for (int i = threadIdx.x; i < (span + 31) / 32; i += blockDim.x) zf_bits[i] = 0u;
     __syncthreads();
@@ -1435,7 +1501,7 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
       int filled = 0;
       for (int b0 = 0; b0 < span && filled < k - cnt; b0 += 64) {
         const int id = b0 + (int)threadIdx.x;
-        const bool fr = id < span && !((zf_bits[id >> 5] >> (id & 31)) & 1u);
+        const bool fr = id < span && id < n_docs && !((zf_bits[id >> 5] >> (id & 31)) & 1u);
         const uint64_t m = __ballot(fr);
         const int pos = filled + (int)__builtin_amdgcn_mbcnt_hi(
                                      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -1519,22 +1585,25 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
   return hipGetLastError();
 }
 
-// Sampling geometry: every P-th tile is a sample tile reporting m keys (the
-// best of each of m doc slices); the first (P, m) in the order P =
-// BM25_SAMPLE_P (default 8), 4, 2 (powers of two), m = 1, 2, 4 whose sample —
-// over the W doc shards searched together (global threshold) — yields >= 2k
-// keys.  P = 1: no threshold — the exact top-4 path over every tile (small
-// indices).  S = keys per query per shard.
+// Sampling geometry: 1 tile in P is a sample tile reporting m keys (the best
+// of each of m doc slices); the first (P, m) in the order P = BM25_SAMPLE_P
+// (default 8), 4, 2 (powers of two), m = 1, 2, 4 whose sample — over the W
+// doc shards searched together (global threshold) — yields >= 2k keys.
+// Sample tiles come in groups of G = 8 consecutive tiles once the index has
+// at least four such groups (G = 1, every P-th tile, below).  P = 1: no
+// threshold — the exact top-4 path over every tile (small indices).  S =
+// keys per query per shard.
 SampleGeom sample_geom(int64_t ntiles, int k, int W) {
   const char* e = getenv("BM25_SAMPLE_P");
   const int pmax = e ? atoi(e) : 8;
   for (int P = 64; P >= 2; P >>= 1) {
     if (P > pmax || ntiles < 2 * P) continue;
-    const int64_t nS = (ntiles + P - 1) / P;
+    const int G = ntiles >= 4 * kSampleGroup * P ? kSampleGroup : 1;
+    const int64_t nS = sample_count(ntiles, P, G);
     for (int m = 1; m <= kTileM; m <<= 1)
-      if (nS * m * W >= 2 * (int64_t)k) return SampleGeom{P, m, nS * m};
+      if (nS * m * W >= 2 * (int64_t)k) return SampleGeom{P, m, nS * m, G};
   }
-  return SampleGeom{1, 0, 0};
+  return SampleGeom{1, 0, 0, 1};
 }
 
 template <int S, int PH, class K>
@@ -1553,6 +1622,13 @@ static int persistent_grid(K kernel) {
 static bool use_pipe(const DevIndex& ix, int64_t T) {
   static const bool off = getenv("BM25_NO_PIPE") != nullptr;
   return !off && T >= 1 && T <= kGroup && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
+}
+
+// Tiles per band of the item order (BM25_BAND overrides, for tuning).
+static int32_t band_tiles() {
+  const char* e = getenv("BM25_BAND");
+  const int v = e ? atoi(e) : kBand;
+  return v >= 1 && v <= 4096 ? v : kBand;
 }
 
 // Item-claim geometry (BM25_CLAIM_CH / BM25_CLAIM_M override, for tuning).
@@ -1595,7 +1671,7 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
   hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG, SM>), dim3((unsigned)grid),
                      dim3(64 * kWaves), 0, st, args_of(ix), q, (int32_t)T, sg.P, sg.nq_host,
                      sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, ws.list, ws.list_cnt, ws.list_cap,
-                     ws.wctr, claim_ch(), claim_m(), sg.cstride, stamps);
+                     ws.wctr, claim_ch(), claim_m(), sg.cstride, sg.G, band_tiles(), stamps);
   if ((DIAG & 32) && PH == kRest) {
     std::vector<uint64_t> h(8 * grid * kWaves);
     hipStreamSynchronize(st);
@@ -1644,6 +1720,7 @@ static Stage main_stage(const DevIndex& ix, int64_t Q, int P, const Workspace& w
   sg.cand_out = ws.cand;
   sg.cstride = ix.ntiles * kTileM;
   sg.P = P;
+  sg.G = 1;
   sg.nt = P > 1 ? 0 : ix.ntiles;
   sg.nq_host = (int32_t)Q;
   if (P > 1) {
@@ -1663,6 +1740,7 @@ static Stage fallback_stage(const DevIndex& ix, int64_t Q, const Workspace& ws) 
   sg.cand_out = ws.cand;
   sg.cstride = ix.ntiles * kTileM;
   sg.P = 1;
+  sg.G = 1;
   sg.nt = ix.ntiles;
   sg.qmap = ws.fb;
   sg.nq_dev = ws.counters + 2;
@@ -1677,6 +1755,7 @@ static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   hipMemsetAsync(keys, 0, sizeof(uint64_t) * Q * g.S, st);
   Stage sg = main_stage(ix, Q, g.P, ws);
   sg.M = g.m;
+  sg.G = g.G;
   sg.cand_out = keys;
   sg.cstride = g.S;
   launch_wave<S_, kSample>(ix, q, T, sg, ws, st);
@@ -1697,7 +1776,7 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   hipMemsetAsync(ws.list_cnt, 0, sizeof(int32_t) * Q, st);
   hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, all_keys,
                      (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap,
-                     ix.nonneg ? 1 : 0);
+                     ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs);
   launch_wave<S_, kRest>(ix, q, T, sg, ws, st);
 }
 
@@ -1745,7 +1824,7 @@ static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k,
                          const Workspace& ws, int32_t* docs, float* scores, hipStream_t st) {
   const int64_t maxflag = maxflag_for(k, sg.nt);
   hipLaunchKernelGGL(merge_first_kernel, dim3((unsigned)sg.nq_host), dim3(kMergeNT), 0, st, sg,
-                     (int32_t)k, maxflag, ix.doc_offset, ws, docs, scores);
+                     (int32_t)k, maxflag, ix.doc_offset, ix.n_docs, ws, docs, scores);
   if (k > kTileM && sg.nt > 0) {  // tiles with exact top-4 candidates may need a rescore
     hipLaunchKernelGGL(rescore_kernel<S>, dim3(256), dim3(kRescoreNT), 0, st, args_of(ix), q,
                        (int32_t)T, (int32_t)k, maxflag, sg, ws);
@@ -1771,7 +1850,11 @@ hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries, int64_t Q
                          int k, int P, const Workspace& ws, int32_t* d_docs, float* d_scores,
                          hipStream_t stream) {
   if (Q == 0 || k == 0) return hipSuccess;
-  if (ix.ntiles == 0) return hipErrorInvalidValue;
+  if (ix.ntiles == 0) {  // an empty doc shard: an all-padding list (doc -1, score bits ~0)
+    hipMemsetAsync(d_docs, 0xFF, sizeof(int32_t) * Q * k, stream);
+    hipMemsetAsync(d_scores, 0xFF, sizeof(float) * Q * k, stream);
+    return hipGetLastError();
+  }
 #define CALL(s) select_s<s>(ix, d_queries, Q, T, k, P, ws, d_docs, d_scores, stream)
   BM25_SHIFT_DISPATCH(CALL)
 #undef CALL

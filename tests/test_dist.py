@@ -1,9 +1,14 @@
-"""The N>1 path on the CPU: world_size-2 ``gloo`` process groups run the
-doc-sharded protocol of bench.py / bm25mi.dist (each rank searches its shard,
-all-gather of the [Q, k] lists, merge by (score desc, doc asc)) and must
-reproduce the single-index top-k bit for bit.  The per-shard search and the
-merge are the oracle's here (no GPU); the GPU merge kernel is covered by
-tests/test_gpu_parity.py::test_sharded_merge_equals_single_index."""
+"""The N>1 path on the CPU: world_size-2 and -3 ``gloo`` process groups run
+the doc-sharded protocol of bench.py / bm25mi.dist and must reproduce the
+single-index top-k bit for bit:
+  * the list exchange (each rank's top-k, all-gather of the [Q, k] lists,
+    merge by (score desc, doc asc));
+  * the global-threshold protocol of bm25mi.dist.sharded_search — sample keys
+    with GLOBAL doc ids, all-gathered by ``gather_keys``, theta = the k-th
+    best, every shard lists its keys >= theta (padded to k), lists gathered
+    and merged — on tie-heavy indices whose tie groups span shards.
+The per-shard scoring is the oracle's here (no GPU); the HIP sample / finish
+/ merge kernels run the same protocol in tests/test_dist_gpu.py."""
 import os
 import socket
 
@@ -94,3 +99,112 @@ def test_single_rank_is_identity():
         assert gd is d and gs is s
     finally:
         dist.destroy_process_group()
+
+
+def _key(score: float, doc: int) -> int:
+    """(score desc, doc asc) as one sortable u64, as bm25mi_internal.h."""
+    u = int(np.float32(score).view(np.uint32))
+    sk = (~u & 0xFFFFFFFF) if u & 0x80000000 else (u | 0x80000000)
+    return (sk << 32) | (0xFFFFFFFF - doc)
+
+
+def _protocol_worker(rank, world, port, args, k, tile, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bm25mi.dist import gather_keys, shard_bounds, sharded_topk
+        from oracle import oracle
+        N, V, Q, T, seed = args
+        ip, ix, dt, q = _tie_index(N, V, Q, T, seed)
+        lo, hi = shard_bounds(N, world, rank, align=tile)
+        sdm = max(b - a for a, b in (shard_bounds(N, world, r, align=tile) for r in range(world)))
+        keys = np.zeros((Q, (sdm + tile - 1) // tile), np.uint64)  # same width on every rank
+        dense = []
+        for i in range(Q):
+            s = np.zeros(hi - lo, np.float32)
+            for t in q[i]:
+                if t < 0:
+                    continue
+                a, b = int(ip[t]), int(ip[t + 1])
+                sel = (ix[a:b] >= lo) & (ix[a:b] < hi)
+                np.add.at(s, ix[a:b][sel] - lo, dt[a:b][sel])
+            dense.append(s)
+            for j in range(0, hi - lo, tile):  # sample: every tile's best, GLOBAL id
+                seg = s[j:j + tile]
+                m = int(np.argmax(seg))
+                keys[i, j // tile] = _key(seg[m], lo + j + m) if seg[m] > 0 else 0
+        all_keys = gather_keys(torch.from_numpy(keys.view(np.int64))).numpy().view(np.uint64)
+        docs = np.full((Q, k), -1, np.int32)
+        scores = np.full((Q, k), np.nan, np.float32)
+        for i in range(Q):
+            ks = np.sort(all_keys[:, i, :].ravel())[::-1]
+            theta = int(ks[k - 1])
+            assert theta != 0, "test index too sparse for the sample"
+            lst = [(_key(v, lo + d), lo + d, v) for d, v in enumerate(dense[i])
+                   if _key(v, lo + d) >= theta]
+            lst.sort(reverse=True)
+            for j, (_, d, v) in enumerate(lst[:k]):
+                docs[i, j], scores[i, j] = d, v
+        gd, gs = sharded_topk(torch.from_numpy(docs), torch.from_numpy(scores), _merge_cpu)
+        if rank == 0:
+            np.savez(result_path, docs=gd.numpy(), scores=gs.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def _tie_index(N, V, Q, T, seed):
+    """Values on a quarter grid (term 0 constant): most scores are tied."""
+    rng = np.random.default_rng(seed)
+    ip, ix, dt = [0], [], []
+    for t in range(V):
+        df = int(rng.integers(N // 10, N // 2))
+        ix.append(np.sort(rng.choice(N, df, replace=False)).astype(np.int32))
+        dt.append(np.full(df, 1.0, np.float32) if t == 0 else
+                  (rng.integers(1, 5, df) / 4).astype(np.float32))
+        ip.append(ip[-1] + df)
+    q = rng.integers(0, V, size=(Q, T)).astype(np.int32)
+    q[0, :] = -1
+    q[0, 0] = 0
+    return np.array(ip, np.int64), np.concatenate(ix), np.concatenate(dt), q
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_global_theta_protocol_ties(tmp_path, world):
+    from oracle import oracle
+    args = (60000, 6, 5, 3, 7)
+    k, tile = 150, 256
+    out = str(tmp_path / "r.npz")
+    mp.spawn(_protocol_worker, args=(world, _free_port(), args, k, tile, out), nprocs=world,
+             join=True)
+    got = np.load(out)
+    ip, ix, dt, q = _tie_index(*args)
+    ref = oracle.search_c(args[0], ip, ix, dt, q, k)
+    assert np.array_equal(got["docs"], ref[0])
+    assert np.array_equal(got["scores"].view(np.uint32), ref[1].view(np.uint32))
+
+
+def _keys_worker(rank, world, port, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bm25mi.dist import gather_keys
+        keys = torch.arange(12, dtype=torch.int64).reshape(3, 4) + 1000 * rank
+        keys[0, 0] = -1 - rank  # u64 keys with the top bit set travel as negative int64
+        g = gather_keys(keys)
+        if rank == 0:
+            np.save(result_path, g.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_gather_keys_rank_major(tmp_path):
+    out = str(tmp_path / "k.npy")
+    mp.spawn(_keys_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    g = np.load(out)
+    assert g.shape == (2, 3, 4)
+    for r in range(2):
+        want = np.arange(12).reshape(3, 4) + 1000 * r
+        want[0, 0] = -1 - r
+        assert np.array_equal(g[r], want)

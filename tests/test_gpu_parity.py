@@ -184,8 +184,10 @@ def test_tiny_and_empty_shapes(gpu):
     assert one.search(np.array([[0]], np.int32), 1)[0].tolist() == [[0]]
 
 
-def test_rescore_path_clustered_tile(gpu):
-    # every high score sits in tile 0, so tile 0 must be rescored exactly
+def test_rescore_path_clustered_tile(gpu, monkeypatch):
+    # every high score sits in tiles 0-2, so the exact path (no sampling) must
+    # rescore them
+    monkeypatch.setenv("BM25_SAMPLE_P", "1")
     N, V = 200_000, 3
     ip = np.array([0, 5000, 5000 + N // 2, 5000 + N // 2 + 10], np.int64)
     ix = np.concatenate([np.arange(5000, dtype=np.int32),
@@ -445,3 +447,65 @@ def test_global_theta_sharded_search(gpu, W):
     merge_topk_device(0, lists_d, lists_s, W, len(q), cfg.k, md, ms, st)
     torch.cuda.synchronize()
     _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)
+
+
+def _doc_slice(indptr, indices, data, lo, hi):
+    """The CSC of documents [lo, hi) (local ids), columns kept."""
+    ip = np.zeros(len(indptr), np.int64)
+    ix, dt = [], []
+    for t in range(len(indptr) - 1):
+        a, b = int(indptr[t]), int(indptr[t + 1])
+        col = indices[a:b]
+        p0, p1 = np.searchsorted(col, lo), np.searchsorted(col, hi)
+        ix.append(col[p0:p1] - lo)
+        dt.append(data[a + p0:a + p1])
+        ip[t + 1] = ip[t] + (p1 - p0)
+    return ip, np.concatenate(ix).astype(np.int32), np.concatenate(dt).astype(np.float32)
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_global_theta_ties_across_shards(gpu, W):
+    """the global threshold is a (score, doc) key; sample
+    keys carry global doc ids and each shard moves theta into its own frame,
+    so a tie group cut by k that spans shards keeps the smallest GLOBAL ids.
+    Columns of constant or quarter-step values make nearly every score tied."""
+    import torch
+    from bm25mi.index import GpuIndex, merge_topk_device
+    from bm25mi.dist import shard_bounds, sharded_search
+    rng = np.random.default_rng(40 + W)
+    N, V = 700_000, 12
+    ip, ix, dt = _rand_index(rng, N, V, 300_000, coarse=True)
+    dt[ip[0]:ip[1]] = 1.0          # term 0: one score everywhere
+    q = np.array([[0, -1, -1], [0, 0, -1], [1, 2, 3], [4, 4, 5], [0, 6, 7], [8, 9, 10]],
+                 np.int32)
+    dq = torch.from_numpy(q).cuda()
+    st = torch.cuda.current_stream()
+    bounds = [shard_bounds(N, W, r) for r in range(W)]
+    sdm = max(hi - lo for lo, hi in bounds)
+    shards = [GpuIndex(*_doc_slice(ip, ix, dt, lo, hi), hi - lo, doc_offset=lo) for lo, hi in bounds]
+    for k in (100, 777):
+        ref = oracle.search_c(N, ip, ix, dt, q, k)
+        keys = []
+        for sh in shards:
+            S = sh.sample_width(k, W, sdm)
+            kk = torch.zeros((len(q), max(S, 1)), dtype=torch.int64, device="cuda")
+            if S > 0:
+                sh.search_sample_device(dq, k, W, sdm, kk, st)
+            keys.append(kk)
+        all_keys = torch.stack(keys)
+
+        class Ex:
+            world = W
+
+            def __call__(self, _):
+                return all_keys
+
+        lists_d = torch.empty((W, len(q), k), dtype=torch.int32, device="cuda")
+        lists_s = torch.empty((W, len(q), k), dtype=torch.float32, device="cuda")
+        for r, sh in enumerate(shards):
+            sharded_search(sh, dq, k, sdm, lists_d[r], lists_s[r], None, st, exchange=Ex())
+        md = torch.empty((len(q), k), dtype=torch.int32, device="cuda")
+        ms = torch.empty((len(q), k), dtype=torch.float32, device="cuda")
+        merge_topk_device(0, lists_d, lists_s, W, len(q), k, md, ms, st)
+        torch.cuda.synchronize()
+        _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)
