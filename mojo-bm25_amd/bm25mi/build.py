@@ -13,7 +13,9 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 REPO = os.path.dirname(os.path.dirname(PKG_DIR))
-LIB = os.path.join(PKG_DIR, "libbm25mi.so")
+# BM25MI_LIB: load a variant build instead (dev timing of compile-time knobs,
+# scripts/build_variant.sh); the product library is always libbm25mi.so.
+LIB = os.environ.get("BM25MI_LIB") or os.path.join(PKG_DIR, "libbm25mi.so")
 SYNTH_LIB = os.path.join(PKG_DIR, "libbm25synth.so")
 
 HIP_SOURCES = ["bm25mi_kernels.hip", "bm25mi_capi.cpp"]
@@ -37,12 +39,13 @@ def _run(cmd, verbose):
 def build(force: bool = False, verbose: bool = False) -> None:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     deps = [os.path.join(CSRC, s) for s in HIP_DEPS] + [os.path.join(REPO, "include", "bm25mi.h")]
-    if force or _stale(LIB, deps):
-        tmp = LIB + ".tmp"
+    lib = os.path.join(PKG_DIR, "libbm25mi.so")
+    if force or _stale(lib, deps):
+        tmp = lib + ".tmp"
         _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
               "-Wno-unused-result", "-Wno-unused-value", "-o", tmp]
              + [os.path.join(CSRC, s) for s in HIP_SOURCES], verbose)
-        os.replace(tmp, LIB)
+        os.replace(tmp, lib)
     sdeps = [os.path.join(CSRC, "synth.cpp")]
     if force or _stale(SYNTH_LIB, sdeps):
         tmp = SYNTH_LIB + ".tmp"

@@ -8,7 +8,8 @@ for d in sys.argv[1:]:
         per = collections.defaultdict(dict)
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            ph = "SAMPLE" if "<11, 1," in name else "REST" if "<11, 2," in name else "ALL" if "<11, 0," in name else name[:30]
+            kind = "band" if "score_band" in name else "pipe"
+            ph = kind + ("_SAMPLE" if "<11, 1," in name else "_REST" if "<11, 2," in name else "_ALL" if "<11, 0," in name else name[:30])
             per[(r["Dispatch_Id"], ph)][r["Counter_Name"]] = float(r["Counter_Value"])
         for (_, ph), cs in per.items():
             for c, v in cs.items():
