@@ -1147,37 +1147,35 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
 // Band score kernel (queries of 1..8 terms; SAMPLE and REST phases).
 //
 // An ITEM is (query, band of up to 8 consecutive phase tiles); a wave scores
-// the band's tiles one after another in its private LDS accumulator.  Why:
-// the score pass is bound by the vector-memory pipe (PMC, config 3, per-tile
-// items: TD busy 98 % of cycles, two thirds of it waiting on L1 misses; ~61
-// L1->L2 requests and ~32 load instructions per tile item), and a third of
-// the per-tile 64-posting rows belonged to LIGHT segments (~9 postings of a
-// term inside a tile, ~5 cache lines per row).  Per band instead:
-//   * the segment table (indptr + rel of every (tile, term)) is loaded once:
-//     lane i * 8 + t holds term t's segment in tile i;
-//   * a LIGHT term — whose postings over the whole band fit in one 128-posting
-//     double row — is loaded once into registers and added tile by tile from
-//     there (lanes outside the tile's segment masked);
-//   * HEAVY terms' postings stream per tile, the next tile's first block
-//     issued before the current tile's adds.
-// Postings move in DOUBLE ROWS: lane l holds postings base + 2l and base +
-// 2l + 1 (base even) — one b32 load of two u16 slots and one 8-byte load of
-// two f32 scores per 128 postings, half the load instructions of 64-posting
-// rows.  Per tile the adds follow the query-term order exactly (light and
-// heavy terms interleaved by term index), so every document's fp32 sum has
-// the reference's rounding sequence (bm25_native.py:152, scipy csc_matvec).
+// the band's tiles one after another in its private LDS accumulator.
+//   * The segment table (indptr + rel of every (tile, term)) is loaded once
+//     per item, one item ahead: lane i * 8 + t holds term t's segment in
+//     tile i.  (Per-tile items load terms, indptr and a rel pair per tile.)
+//   * Postings move in DOUBLE ROWS: lane l holds postings base + 2l and
+//     base + 2l + 1 (base even) — one b32 load of two u16 slots and one
+//     8-byte load of two f32 scores per 128 postings, half the load
+//     instructions of 64-posting rows.
+//   * Every tile iteration issues the SAME loads: the next tile's first two
+//     blocks of kJ2 double rows (rows past its end read posting 0), so the
+//     compiler's vmcnt waits are exact counts; a load issued under a branch
+//     and still in flight makes every later wait drain it (LLVM merges the
+//     paths pessimistically), which is what exposed the per-tile kernel's
+//     second row block.  The next item's first tile is issued during the
+//     current item's last tile.
+// Per tile the adds follow the query-term order exactly, so every document's
+// fp32 sum has the reference's rounding sequence (bm25_native.py:152, scipy
+// csc_matvec).
 // ===========================================================================
 constexpr int kBandT = 8;    // terms served (T <= kBandT)
-#ifndef BM25_BANDL
-#define BM25_BANDL 4
-#endif
-constexpr int kBandL = BM25_BANDL;  // light terms cached per band item
-constexpr int kBandLA = kBandL > 0 ? kBandL : 1;  // (array extent)
 constexpr int kBandW = 8;    // tiles per band item
 #ifndef BM25_KJ2
 #define BM25_KJ2 3
 #endif
 constexpr int kJ2 = BM25_KJ2;  // double rows per streamed block
+#ifndef BM25_NB
+#define BM25_NB 2
+#endif
+constexpr int kNB = BM25_NB;   // blocks of the next tile issued one tile ahead
 
 struct BandDesc {  // lane i * 8 + t: term t's segment bounds in tile i (raw)
   uint32_t ip, r0, r1;  // indptr[term] (nnz < 2^30 on this path), rel pair
@@ -1189,7 +1187,15 @@ struct BandCur {  // XCD-relative item ordinal, its chunk end, band, query, band
   int32_t rit, end, b, q, bw;
 };
 
-// A tile's heavy double rows: lane j of the table describes row j0 + j.
+struct BandTab {  // an item's segment table (lane i * 8 + t) and its threshold
+  uint32_t sb, sl;  // segment [sb, sb + sl) of the posting arrays (sl = 0: none)
+  uint64_t th;      // REST: theta of the item's query
+};
+
+// Row base of the rows past a table's end (issue_rows2).
+constexpr uint32_t kNoRow = 0u;
+
+// A tile's double rows: lane j of the table describes row j0 + j.
 struct Rows2 {
   uint32_t base;    // even posting index of the row's first posting pair
   uint32_t lo, hi;  // the row's term segment [lo, hi): its valid postings
@@ -1197,8 +1203,8 @@ struct Rows2 {
   uint32_t nrows;   // rows of the tile (uniform)
 };
 
-// Heavy segment of term s (lane s < T): [beg, beg + len), cut into double
-// rows from beg & ~1.
+// Segment of term s (lane s < T): [beg, beg + len), cut into double rows from
+// beg & ~1.
 __device__ __forceinline__ Rows2 make_rows2(uint32_t beg, uint32_t len, int T, uint32_t j0) {
   const uint32_t lane = lane_id();
   len = (int)lane < T ? len : 0u;
@@ -1219,7 +1225,7 @@ __device__ __forceinline__ Rows2 make_rows2(uint32_t beg, uint32_t len, int T, u
   const uint32_t b = (uint32_t)__shfl((int)beg, pos, 64);
   const uint32_t l = (uint32_t)__shfl((int)len, pos, 64);
   const bool in = j < r.nrows;
-  r.base = in ? (b & ~1u) + 128u * (j - st) : 0u;
+  r.base = in ? (b & ~1u) + 128u * (j - st) : kNoRow;
   r.lo = in ? b : 1u;
   r.hi = in ? b + l : 0u;
   r.term = in ? (uint32_t)pos : (uint32_t)T;
@@ -1227,7 +1233,10 @@ __device__ __forceinline__ Rows2 make_rows2(uint32_t beg, uint32_t len, int T, u
 }
 
 // Loads of double rows [j0, j0 + kJ2) of a table: slot pair + score pair per
-// lane (every load issued; rows past the table read posting 0 and are masked).
+// lane.  Every load is issued (static counts); rows past the table read
+// posting 0 (an L1 hit) and are masked later.  (Loading them through a
+// descriptor of zero records instead — range-checked, no memory access — ran
+// the config-3 score pass slower: 5.12 vs 4.75 ms.)
 __device__ __forceinline__ void issue_rows2(const PostingRsrc& pr, const Rows2& R, int j0,
                                             uint32_t (&ld)[kJ2], float (&v0)[kJ2],
                                             float (&v1)[kJ2]) {
@@ -1320,12 +1329,28 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     d.r0 = r[0];
     d.r1 = r[1];
     d.ok = ok ? 1u : 0u;
-    d.skey = ~0ull;
-    if (skipping && (c.b % P) == 0) {
-      const int64_t si = (int64_t)(c.b / P) * kBandW + min(li, (uint32_t)(c.bw - 1));
-      d.skey = skeys[(int64_t)c.q * sstride + si];
-    }
+    const int64_t si = (int64_t)(c.b / P) * kBandW + min(li, (uint32_t)(c.bw - 1));
+    d.skey = skipping ? skeys[(int64_t)c.q * sstride + min<int64_t>(si, sstride - 1)] : ~0ull;
+    if (!(skipping && (c.b % P) == 0)) d.skey = ~0ull;
     return d;
+  };
+  // the item's table; REST: a sample tile whose best key scores below theta
+  // holds no key of the list, so its segments are dropped (exact for m = 1
+  // samples; only when theta is a positive score — no threshold and the
+  // zero-fill case must still see every doc)
+  auto make_tab = [&](const BandDesc& d, uint64_t th) -> BandTab {
+    BandTab tb;
+    const bool th_pos = PH == kRest && (uint32_t)(th >> 32) > score_key(0.f);
+    const bool skip = skipping && th_pos && (uint32_t)(d.skey >> 32) < (uint32_t)(th >> 32);
+    tb.sb = d.ip + d.r0;
+    tb.sl = (d.ok && !skip) ? d.r1 - d.r0 : 0u;
+    tb.th = th;
+    return tb;
+  };
+  auto tile_rows = [&](const BandTab& tb, int i, uint32_t j0) -> Rows2 {
+    const int src = i * 8 + (int)lt;
+    return make_rows2((uint32_t)__shfl((int)tb.sb, src, 64), (uint32_t)__shfl((int)tb.sl, src, 64),
+                      T, j0);
   };
 
   BandCur c0;
@@ -1333,143 +1358,68 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
   c0.end = 0;
   c0.b = c0.q = 0;
   c0.bw = 1;
-  BandCur cN = next(c0);
-  if (cN.rit >= ngi) return;
+  BandCur cur = next(c0);
+  if (cur.rit >= ngi) return;
   zero_acc<S>(acc);
   acc[D + lane] = 0.f;
-  BandCur cN1 = next(cN), cN2 = next(cN1);
-  int32_t tmN1 = terms_of(cN1);
-  BandDesc dN = load_bdesc(cN, terms_of(cN));
-  uint64_t thN = PH == kRest ? theta[cN.q] : 0ull;
-
-  while (cN.rit < ngi) {
-    const BandCur c = cN;
-    const BandDesc d = dN;
-    const uint64_t th = thN;
-    // ---- the next items' loads: terms two items ahead, segment table one
-    const int32_t tmN2 = terms_of(cN2);
-    dN = load_bdesc(cN1, tmN1);
-    thN = PH == kRest ? theta[cN1.q] : 0ull;
-
-    // ---- this item's segment table
-    const float thf_raw = key_score((uint32_t)(th >> 32));
-    const bool th_pos = PH == kRest && (uint32_t)(th >> 32) > score_key(0.f);
-    // REST: a sample tile whose best key scores below theta holds no key of
-    // the list: its segments are emptied (exact for m = 1; th_pos excludes
-    // the cases — no threshold — that must still see every doc)
-    const bool skip = skipping && th_pos && (uint32_t)(d.skey >> 32) < (uint32_t)(th >> 32);
-    const uint32_t sb = d.ip + d.r0;
-    const uint32_t sl = (d.ok && !skip) ? d.r1 - d.r0 : 0u;
-    // term t's span over the band (lanes of equal t: stride 8)
-    uint32_t slo = sl ? sb : 0xFFFFFFFFu, shi = sl ? sb + sl : 0u;
+  // prologue: the first item's table (one exposed load chain), the next
+  // item's descriptors in flight
+  BandTab tab = make_tab(load_bdesc(cur, terms_of(cur)), PH == kRest ? theta[cur.q] : 0ull);
+  BandCur nx = next(cur);
+  BandDesc dN = load_bdesc(nx, terms_of(nx));
+  uint64_t thN = PH == kRest ? theta[nx.q] : 0ull;
+  BandCur nx2 = next(nx);
+  int32_t tmN2 = terms_of(nx2);
+  Rows2 rD = tile_rows(tab, 0, 0);
+  uint32_t ltD[kNB][kJ2];
+  float vD0[kNB][kJ2], vD1[kNB][kJ2];
 #pragma unroll
-    for (int m = 8; m < 64; m <<= 1) {
-      slo = min(slo, (uint32_t)__shfl_xor((int)slo, m, 64));
-      shi = max(shi, (uint32_t)__shfl_xor((int)shi, m, 64));
-    }
-    const bool light_l = shi > slo && shi - (slo & ~1u) <= 128u;
-    // the first kBandL light terms are cached (cache slot u holds term lt_[u]);
-    // further light terms stream like heavy ones
-    uint32_t lightm = (uint32_t)(__ballot(lane < 8 && light_l) & 0xFFu);
-    int lt_[kBandLA];
-    {
-      uint32_t m = lightm, keep = 0;
-#pragma unroll
-      for (int u = 0; u < kBandL; ++u) {
-        lt_[u] = m ? __builtin_ctz(m) : kBandT;
-        keep |= m & (0u - m);
-        m &= m - 1u;
-      }
-      lightm = keep;
-    }
-    // heavy (term, tile) segments only, for the per-tile row tables
-    const uint32_t slh = ((lightm >> lt) & 1u) ? 0u : sl;
+  for (int k = 0; k < kNB; ++k) issue_rows2(pr, rD, k * kJ2, ltD[k], vD0[k], vD1[k]);
+  BandCur nx3 = nx2;
+  int32_t tmN3 = tmN2;
 
-    // ---- cached light terms: one double row per band
-    uint32_t ls[kBandLA];
-    float lv0[kBandLA], lv1[kBandLA];
-    // first posting (even) of term t's double row
-    auto la = [&](int t) -> uint32_t { return lane_u32(slo, t) & ~1u; };
-#pragma unroll
-    for (int u = 0; u < kBandL; ++u) {
-      ls[u] = 0u;
-      lv0[u] = lv1[u] = 0.f;
-      if (lt_[u] < kBandT) {
-        const uint32_t a0 = la(lt_[u]);
-        ls[u] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)(lane * 4u), (int)(a0 * 2u), 0);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)(lane * 8u), (int)(a0 * 4u), 0);
-        lv0[u] = __uint_as_float((uint32_t)v[0]);
-        lv1[u] = __uint_as_float((uint32_t)v[1]);
-      }
-    }
-    // heavy row table of tile i (lane t: term t's heavy segment in tile i)
-    auto tile_rows = [&](int i, uint32_t j0) -> Rows2 {
-      const int src = i * 8 + (int)lt;
-      return make_rows2((uint32_t)__shfl((int)sb, src, 64), (uint32_t)__shfl((int)slh, src, 64),
-                        T, j0);
-    };
-    Rows2 rD = tile_rows(0, 0);
-    uint32_t ltD[kJ2];
-    float vD0[kJ2], vD1[kJ2];
-    issue_rows2(pr, rD, 0, ltD, vD0, vD1);
-
-    for (int i = 0; i < c.bw; ++i) {
-      const int64_t tile = tile_of32<PH>((uint32_t)(c.b * kBandW + i), (uint32_t)P, (uint32_t)G);
-      const int64_t ti = (int64_t)c.b * kBandW + i;  // phase tile (SAMPLE: sample index)
+  while (cur.rit < ngi) {
+    BandTab ntab = tab;
+    for (int i = 0; i < cur.bw; ++i) {
+      const bool last = i + 1 == cur.bw;
+      const int64_t ti = (int64_t)cur.b * kBandW + i;  // phase tile (SAMPLE: sample index)
+      const int64_t tile = tile_of32<PH>((uint32_t)ti, (uint32_t)P, (uint32_t)G);
       const uint32_t nrD = rD.nrows;
-      uint32_t ltX[kJ2];
-      float vX0[kJ2], vX1[kJ2];
-      if (nrD > kJ2) issue_rows2(pr, rD, kJ2, ltX, vX0, vX1);
-      Rows2 rC = rD;
-      uint32_t ltC[kJ2];
-      float vC0[kJ2], vC1[kJ2];
-      if (i + 1 < c.bw) {
-        rC = tile_rows(i + 1, 0);
-        issue_rows2(pr, rC, 0, ltC, vC0, vC1);
+      // ---- on the item's last tile: the next item's table (descriptors
+      // loaded one item ago), the descriptors of the one after it and the
+      // terms of the one after that (claims are consumed here, where only
+      // this tile's old row blocks are in flight)
+      if (last) {
+        nx3 = next(nx2);
+        tmN3 = terms_of(nx3);
+        ntab = make_tab(dN, thN);
+        dN = load_bdesc(nx2, tmN2);
+        thN = PH == kRest ? theta[nx2.q] : 0ull;
       }
+      // ---- the next tile's first kNB blocks (of this item or the next)
+      Rows2 rC = last ? tile_rows(ntab, 0, 0) : tile_rows(tab, i + 1, 0);
+      if (last && nx.rit >= ngi) rC.nrows = 0;
+      uint32_t ltC[kNB][kJ2];
+      float vC0[kNB][kJ2], vC1[kNB][kJ2];
+#pragma unroll
+      for (int k = 0; k < kNB; ++k) issue_rows2(pr, rC, k * kJ2, ltC[k], vC0[k], vC1[k]);
+
+      const uint64_t th = tab.th;
+      const float thf_raw = key_score((uint32_t)(th >> 32));
+      const bool th_pos = PH == kRest && (uint32_t)(th >> 32) > score_key(0.f);
       // REST over a non-negative index: candidates are flagged while adding
       const bool flagged = PH == kRest && a.nonneg && th_pos;
       const float thf = flagged ? thf_raw : __builtin_nanf("");
       uint64_t hit = 0;
-      // one posting pair per lane: postings p and p + 1 of [l0, l1) are added
-      // at their slots, the rest go to the lane's trash slot with score 0;
-      // returns the masked slot pair (for the emission)
-      auto rmw_pair = [&](uint32_t p, uint32_t slots, float v0, float v1, uint32_t l0,
-                          uint32_t l1) -> uint32_t {
-        const bool m0 = p >= l0 && p < l1, m1 = p + 1u >= l0 && p + 1u < l1;
-        const uint32_t d0 = m0 ? (slots & 0xFFFFu) : trash;
-        const uint32_t d1 = m1 ? (slots >> 16) : trash;
-        const float x0 = acc[d0], x1 = acc[d1];  // distinct docs (one term)
-        const float y0 = x0 + (m0 ? v0 : 0.f), y1 = x1 + (m1 ? v1 : 0.f);
-        acc[d0] = y0;
-        acc[d1] = y1;
-        hit |= __ballot(y0 >= thf) | __ballot(y1 >= thf);
-        return d0 | (d1 << 16);
-      };
-      // ---- adds, in query-term order
-      int tdone = -1;
-      auto light_upto = [&](int tu) {  // cached light terms tdone+1 .. tu-1, in order
-#pragma unroll
-        for (int u = 0; u < kBandL; ++u) {
-          const int t = lt_[u];
-          if (t > tdone && t < tu) {
-            const uint32_t l0 = lane_u32(sb, i * 8 + t), l1 = l0 + lane_u32(sl, i * 8 + t);
-            if (l1 > l0) rmw_pair(la(t) + 2u * lane, ls[u], lv0[u], lv1[u], l0, l1);
-          }
-        }
-        tdone = max(tdone, tu - 1);
-      };
-      // a block of heavy double rows j0.. (n of them), each preceded by the
-      // light terms before it; the masked slot pairs replace the loaded ones
-      auto heavy_block = [&](const Rows2& R, int j0, uint32_t (&ld)[kJ2], float (&v0)[kJ2],
-                             float (&v1)[kJ2], uint32_t n) {
-        // masked slot pairs and scores first; then per row read-add-write,
-        // the next row's reads issued before this row's writes when both rows
-        // are of one term (distinct docs), after them otherwise (term order)
+      // ---- adds in row order (= query-term order: a term's rows are
+      // consecutive); the next row's reads go before this row's writes when
+      // both rows are of one term (distinct docs), after them otherwise
+      auto block = [&](const Rows2& R, int j0, uint32_t (&ld)[kJ2], float (&v0)[kJ2],
+                       float (&v1)[kJ2], uint32_t n) {
         int tm[kJ2];
 #pragma unroll
         for (int j = 0; j < kJ2; ++j) {
-          tm[j] = (uint32_t)j < n ? (int)lane_u32(R.term, j0 + j) : kBandT;
+          tm[j] = (uint32_t)j < n ? (int)lane_u32(R.term, j0 + j) : -1 - j;
           const uint32_t p = lane_u32(R.base, j0 + j) + 2u * lane;
           const uint32_t l0 = lane_u32(R.lo, j0 + j), l1 = lane_u32(R.hi, j0 + j);
           const bool m0 = p >= l0 && p < l1, m1 = p + 1u >= l0 && p + 1u < l1;
@@ -1478,8 +1428,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
           v1[j] = m1 ? v1[j] : 0.f;
         }
         if (n == 0) return;
-        light_upto(tm[0]);
-        tdone = tm[0];
         float x0 = acc[ld[0] & 0xFFFFu], x1 = acc[ld[0] >> 16];
 #pragma unroll
         for (int j = 0; j < kJ2; ++j) {
@@ -1495,8 +1443,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
             acc[ld[j] >> 16] = y1;
             hit |= __ballot(y0 >= thf) | __ballot(y1 >= thf);
             if (j + 1 < kJ2 && (uint32_t)(j + 1) < n && !same) {
-              light_upto(tm[j + 1]);
-              tdone = tm[j + 1];
               n0 = acc[ld[j + 1] & 0xFFFFu];
               n1 = acc[ld[j + 1] >> 16];
             }
@@ -1505,26 +1451,31 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
           }
         }
       };
-      heavy_block(rD, 0, ltD, vD0, vD1, min(nrD, (uint32_t)kJ2));
-      if (nrD > kJ2) heavy_block(rD, kJ2, ltX, vX0, vX1, min(nrD - kJ2, (uint32_t)kJ2));
-      if (nrD > 2 * kJ2) {
-        // ---- a heavy tile: the remaining rows, block j + kJ2 issued before
-        // block j; dense selection (the D/X slot pairs are dead here)
+#pragma unroll
+      for (int k = 0; k < kNB; ++k)
+        block(rD, k * kJ2, ltD[k], vD0[k], vD1[k],
+              nrD > (uint32_t)(k * kJ2) ? min(nrD - k * kJ2, (uint32_t)kJ2) : 0u);
+
+      if (nrD > kNB * kJ2) {
+        // ---- a heavy tile: the remaining rows, block j + kJ2 always issued
+        // before block j's adds (past the end: posting 0); dense selection
         Rows2 t = rD;
-        if ((2 * kJ2 & 63) == 0) t = tile_rows(i, 2 * kJ2);
+        if (((kNB * kJ2) & 63) == 0) t = tile_rows(tab, i, kNB * kJ2);
         uint32_t ltY[kJ2];
         float vY0[kJ2], vY1[kJ2];
-        issue_rows2(pr, t, (2 * kJ2) & 63, ltY, vY0, vY1);
-        for (uint32_t j = 2 * kJ2; j < nrD; j += kJ2) {
+        issue_rows2(pr, t, (kNB * kJ2) & 63, ltY, vY0, vY1);
+        for (uint32_t j = kNB * kJ2; j < nrD; j += kJ2) {
           const uint32_t jn = j + kJ2;
           Rows2 tn = t;
+          if (jn < nrD && (jn & 63) == 0) tn = tile_rows(tab, i, jn);
+          if (jn >= nrD) {  // nothing left: a dead block keeps the load count static
+            tn.base = kNoRow;
+            tn.hi = 0u;
+          }
           uint32_t ltZ[kJ2];
           float vZ0[kJ2], vZ1[kJ2];
-          if (jn < nrD) {
-            if ((jn & 63) == 0) tn = tile_rows(i, jn);
-            issue_rows2(pr, tn, (int)(jn & 63), ltZ, vZ0, vZ1);
-          }
-          heavy_block(t, (int)(j & 63), ltY, vY0, vY1, min(nrD - j, (uint32_t)kJ2));
+          issue_rows2(pr, tn, (int)(jn & 63), ltZ, vZ0, vZ1);
+          block(t, (int)(j & 63), ltY, vY0, vY1, min(nrD - j, (uint32_t)kJ2));
           t = tn;
 #pragma unroll
           for (int u = 0; u < kJ2; ++u) {
@@ -1533,72 +1484,49 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
             vY1[u] = vZ1[u];
           }
         }
-        light_upto(kBandT);
-        if (PH == kRest && a.nonneg && th_pos && hit == 0)
+        if (flagged && hit == 0)
           zero_acc<S>(acc);
         else if (PH == kRest)
-          emit_rest<S>(acc, tile, a.n_docs, th, list + (int64_t)c.q * C, list_cnt + c.q, C);
+          emit_rest<S>(acc, tile, a.n_docs, th, list + (int64_t)cur.q * C, list_cnt + cur.q, C);
         else
           best_dense<S, SM>(acc, tile, a.n_docs, (uint32_t)a.doc_offset,
-                            cand + (int64_t)c.q * cstride + ti * SM);
+                            cand + (int64_t)cur.q * cstride + ti * SM);
       } else {
-        light_upto(kBandT);
-
-        // ---- selection / emission of tile i from its touched slots; the
-        // accumulator is left zeroed
-        // every touched slot of the tile: heavy rows' masked
-        // slot pairs, then the light rows masked to the tile's segments
+        // ---- selection / emission from the touched slots (the D blocks'
+        // masked slot pairs); the accumulator is left zeroed
         auto for_ops = [&](auto&& f) {
-          const uint32_t n0 = min(nrD, (uint32_t)kJ2), n1 = nrD > kJ2 ? nrD - kJ2 : 0u;
 #pragma unroll
-          for (int j = 0; j < kJ2; ++j)
-            if ((uint32_t)j < n0) {
-              f(ltD[j] & 0xFFFFu);
-              f(ltD[j] >> 16);
-            }
+          for (int k = 0; k < kNB; ++k)
 #pragma unroll
-          for (int j = 0; j < kJ2; ++j)
-            if ((uint32_t)j < n1) {
-              f(ltX[j] & 0xFFFFu);
-              f(ltX[j] >> 16);
-            }
-#pragma unroll
-          for (int u = 0; u < kBandL; ++u) {
-            const int t = lt_[u];
-            if (t < kBandT) {
-              const uint32_t l0 = lane_u32(sb, i * 8 + t), l1 = l0 + lane_u32(sl, i * 8 + t);
-              if (l1 > l0) {
-                const uint32_t p = la(t) + 2u * lane;
-                f((p >= l0 && p < l1) ? (ls[u] & 0xFFFFu) : trash);
-                f((p + 1u >= l0 && p + 1u < l1) ? (ls[u] >> 16) : trash);
+            for (int j = 0; j < kJ2; ++j)
+              if ((uint32_t)(k * kJ2 + j) < nrD) {
+                f(ltD[k][j] & 0xFFFFu);
+                f(ltD[k][j] >> 16);
               }
-            }
-          }
         };
         auto clear_ops = [&]() { for_ops([&](uint32_t s) { acc[s] = 0.f; }); };
         if (flagged && hit == 0) {  // no doc of this tile reaches theta
           clear_ops();
         } else if (PH == kRest && th_pos && a.nonneg) {
-          // two passes over the touched slots: count (a passing sum is marked
-          // by negating it — sums are >= 0 here — so a doc reached through two
-          // slots counts once), then write the marked ones in the same order
-          const float thv = thf_raw;
+          // two passes: count (a passing sum is marked by negating it — sums
+          // are >= 0 here — so a doc reached twice counts once), then write
+          // the marked ones in the same order
           const int64_t base = tile << S;
           const int tie = (int)max<int64_t>(
               -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)th) - base + 1));
           int cnt = 0;
           for_ops([&](uint32_t s) {
             const float x = acc[s];
-            const bool pass = (x > thv) | ((x == thv) & ((int)s < tie));
+            const bool pass = (x > thf_raw) | ((x == thf_raw) & ((int)s < tie));
             if (pass) acc[s] = -x;
             cnt += pass;
           });
           if (__ballot(cnt > 0) != 0) {
             const uint32_t incl = wave_incl_scan((uint32_t)cnt);
             int pos = 0;
-            if (lane == 63) pos = atomicAdd(list_cnt + c.q, (int)incl);
+            if (lane == 63) pos = atomicAdd(list_cnt + cur.q, (int)incl);
             pos = __shfl(pos, 63, 64) + (int)incl - cnt;
-            uint64_t* lq = list + (int64_t)c.q * C;
+            uint64_t* lq = list + (int64_t)cur.q * C;
             for_ops([&](uint32_t s) {
               const float x = acc[s];
               if (x < 0.f) {
@@ -1611,58 +1539,60 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
           }
           clear_ops();
         } else if (PH == kRest) {
-          emit_rest<S>(acc, tile, a.n_docs, th, list + (int64_t)c.q * C, list_cnt + c.q, C);
+          emit_rest<S>(acc, tile, a.n_docs, th, list + (int64_t)cur.q * C, list_cnt + cur.q, C);
         } else {  // SAMPLE: the best key of each of SM doc slices of the tile
-          uint64_t* out = cand + (int64_t)c.q * cstride + ti * SM;
-          {
-            const int sh = S - (SM == 1 ? 0 : (SM == 2 ? 1 : 2));
-            uint32_t bk[SM], bd[SM];
+          const int sh = S - (SM == 1 ? 0 : (SM == 2 ? 1 : 2));
+          uint32_t bk[SM], bd[SM];
+#pragma unroll
+          for (int u = 0; u < SM; ++u) {
+            bk[u] = 0;
+            bd[u] = 0xFFFFFFFFu;
+          }
+          for_ops([&](uint32_t s) {
+            const float x = acc[s];
+            const uint32_t key = (x > 0.f && s < (uint32_t)D) ? score_key(x) : 0u;
+            const uint32_t sli = SM == 1 ? 0u : (s >> sh);
 #pragma unroll
             for (int u = 0; u < SM; ++u) {
-              bk[u] = 0;
-              bd[u] = 0xFFFFFFFFu;
+              const bool better =
+                  sli == (uint32_t)u && (key > bk[u] || (key == bk[u] && key != 0u && s < bd[u]));
+              bd[u] = better ? s : bd[u];
+              bk[u] = better ? key : bk[u];
             }
-            for_ops([&](uint32_t s) {
-              const float x = acc[s];
-              const uint32_t key = (x > 0.f && s < (uint32_t)D) ? score_key(x) : 0u;
-              const uint32_t sli = SM == 1 ? 0u : (s >> sh);
+          });
+          clear_ops();
+          const uint32_t base = (uint32_t)(tile << S) + (uint32_t)a.doc_offset;
+          uint64_t* out = cand + (int64_t)cur.q * cstride + ti * SM;
 #pragma unroll
-              for (int u = 0; u < SM; ++u) {
-                const bool better =
-                    sli == (uint32_t)u && (key > bk[u] || (key == bk[u] && key != 0u && s < bd[u]));
-                bd[u] = better ? s : bd[u];
-                bk[u] = better ? key : bk[u];
-              }
-            });
-            clear_ops();
-            const uint32_t base = (uint32_t)(tile << S) + (uint32_t)a.doc_offset;
-#pragma unroll
-            for (int u = 0; u < SM; ++u) {
-              const uint32_t wm = wave_max_u32(bk[u]);
-              uint64_t key = 0ull;
-              if (wm != 0) {
-                const uint32_t doc =
-                    0xFFFFFFFFu - wave_max_u32(bk[u] == wm ? 0xFFFFFFFFu - bd[u] : 0u);
-                key = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (base + doc));
-              }
-              if (lane == 0) out[u] = key;
+          for (int u = 0; u < SM; ++u) {
+            const uint32_t wm = wave_max_u32(bk[u]);
+            uint64_t key = 0ull;
+            if (wm != 0) {
+              const uint32_t doc =
+                  0xFFFFFFFFu - wave_max_u32(bk[u] == wm ? 0xFFFFFFFFu - bd[u] : 0u);
+              key = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (base + doc));
             }
+            if (lane == 0) out[u] = key;
           }
         }
       }
       // ---- rotate
       rD = rC;
 #pragma unroll
-      for (int j = 0; j < kJ2; ++j) {
-        ltD[j] = ltC[j];
-        vD0[j] = vC0[j];
-        vD1[j] = vC1[j];
-      }
+      for (int k = 0; k < kNB; ++k)
+#pragma unroll
+        for (int j = 0; j < kJ2; ++j) {
+          ltD[k][j] = ltC[k][j];
+          vD0[k][j] = vC0[k][j];
+          vD1[k][j] = vC1[k][j];
+        }
     }
-    cN = cN1;
-    cN1 = cN2;
-    cN2 = next(cN2);
-    tmN1 = tmN2;
+    // ---- next item (its first tile is in flight)
+    tab = ntab;
+    cur = nx;
+    nx = nx2;
+    nx2 = nx3;
+    tmN2 = tmN3;
   }
 }
 
@@ -2218,11 +2148,11 @@ static int32_t band_claim() {
   return v >= 1 && v <= 64 ? v : 1;
 }
 
-// The band kernel can serve SAMPLE and REST for queries of 1..8 terms; it is
-// opt-in (BM25_BAND_KERNEL=1) while it trails the per-tile pipelined kernel.
+// The band kernel serves SAMPLE and REST for queries of 1..8 terms
+// (BM25_NO_BAND=1 forces the per-tile pipelined kernel).
 static bool use_band(const DevIndex& ix, int64_t T) {
-  static const bool on = getenv("BM25_BAND_KERNEL") != nullptr;
-  return on && T >= 1 && T <= kBandT && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
+  static const bool off = getenv("BM25_NO_BAND") != nullptr;
+  return !off && T >= 1 && T <= kBandT && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
 }
 
 template <int S, int PH, int SM = 1>

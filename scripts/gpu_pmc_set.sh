@@ -9,7 +9,7 @@ i=0
 while read -r ctrs; do
   [ -z "$ctrs" ] && continue
   i=$((i+1))
-  timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-include-regex "score_(pipe|band)" --output-format csv -d $OUT/pmcs_p$i -o pmc -- python3 $R/scripts/ablate.py ${CFG:-c3} > $OUT/pmcs_p$i.log 2>&1 || exit $?
+  env ${PMC_ENV} timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-include-regex "score_(pipe|band)" --output-format csv -d $OUT/pmcs_p$i -o pmc -- python3 $R/scripts/ablate.py ${CFG:-c3} > $OUT/pmcs_p$i.log 2>&1 || exit $?
 done <<'CTRS'
 TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum
 TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE GRBM_COUNT
