@@ -21,9 +21,13 @@
  *     KATs test_topk.mojo:222-238).  Parity with bm25_native itself is pinned
  *     by tests/golden/ (tie-aware: ids exact where the score is untied).
  *
- * Build: gcc -O2 -ffp-contract=off -fPIC -shared (oracle/Makefile); no
+ * oracle_search_mt splits the query batch over POSIX threads (each with its
+ * own accumulator); per query it is the same computation.
+ *
+ * Build: gcc -O2 -ffp-contract=off -fPIC -shared -pthread (oracle/Makefile); no
  * -ffast-math: the adds must stay IEEE fp32, unreordered.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -116,5 +120,62 @@ int oracle_search(int64_t n_docs, int64_t n_terms, const int64_t* indptr, const 
     if (rc == 0) rc = oracle_topk(acc, n_docs, k, out_docs + q * k, out_scores + q * k);
   }
   free(acc);
+  return rc;
+}
+
+/* the same batched search with the queries split over n_threads threads */
+typedef struct {
+  int64_t n_docs, n_terms;
+  const int64_t* indptr;
+  const int32_t* indices;
+  const float* data;
+  const int32_t* queries;
+  int64_t q0, q1, T;
+  int32_t k;
+  int32_t* out_docs;
+  float* out_scores;
+  int rc;
+} oracle_job;
+
+static void* oracle_job_run(void* p) {
+  oracle_job* j = (oracle_job*)p;
+  j->rc = oracle_search(j->n_docs, j->n_terms, j->indptr, j->indices, j->data,
+                        j->queries + j->q0 * j->T, j->q1 - j->q0, j->T, j->k,
+                        j->out_docs + j->q0 * j->k, j->out_scores + j->q0 * j->k);
+  return NULL;
+}
+
+int oracle_search_mt(int64_t n_docs, int64_t n_terms, const int64_t* indptr,
+                     const int32_t* indices, const float* data, const int32_t* queries, int64_t Q,
+                     int64_t T, int32_t k, int32_t* out_docs, float* out_scores, int n_threads) {
+  if (k < 0 || k > n_docs) return 1;
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > Q) n_threads = Q > 0 ? (int)Q : 1;
+  oracle_job* jobs = (oracle_job*)calloc((size_t)n_threads, sizeof(oracle_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));
+  if (!jobs || !th) {
+    free(jobs);
+    free(th);
+    return 2;
+  }
+  int rc = 0;
+  for (int i = 0; i < n_threads; ++i) {
+    oracle_job* j = &jobs[i];
+    j->n_docs = n_docs; j->n_terms = n_terms; j->indptr = indptr; j->indices = indices;
+    j->data = data; j->queries = queries; j->T = T; j->k = k;
+    j->out_docs = out_docs; j->out_scores = out_scores;
+    j->q0 = Q * i / n_threads;
+    j->q1 = Q * (i + 1) / n_threads;
+    if (pthread_create(&th[i], NULL, oracle_job_run, j) != 0) {
+      j->rc = 2;
+      th[i] = 0;
+    }
+  }
+  for (int i = 0; i < n_threads; ++i) {
+    if (th[i]) pthread_join(th[i], NULL);
+    if (jobs[i].rc && !rc) rc = jobs[i].rc;
+  }
+  free(jobs);
+  free(th);
   return rc;
 }
