@@ -13,10 +13,14 @@ it, and the per-shard [Q, k] lists are all-gathered and merged on the GPU, so
 every step returns the same global top-k as one GPU would.  Total work is fixed as N
 grows ("scaling": "strong").
 
-Printed by rank 0: ONE JSON line with the metric, the roofline of the
-dominant kernel (score_tiles, timed with HIP events on its stream over the
-timed region) and the CPU baseline (the reference's scipy/numpy call
-sequence, oracle.search_faithful, on a bounded query sample, rank 0 at N=1).
+Printed by rank 0: ONE JSON line with the metric (value = steps x Q / the
+barrier-bracketed wall time, max over ranks), the per-step median from HIP
+events, the roofline of the dominant kernel (the score pass, timed with HIP
+events on its stream over the timed region), the end-to-end host-buffer time
+(bm25_search: H2D queries -> D2H results, median of --e2e-batches, N=1) and
+the CPU baseline (the reference's scipy/numpy call sequence,
+oracle.search_faithful, on a seeded 64-query sample: one process, and a fork
+pool over the job's cores; rank 0 at N=1, run before the GPU is touched).
 """
 from __future__ import annotations
 
@@ -74,14 +78,58 @@ def load_traffic(path: str, config: str, shift: int):
     return None
 
 
+def cpu_baseline(args, n_docs, indptr, indices, data, queries, k):
+    """BASELINE.md CPU legs on a seeded query sample: (i) one process, one
+    core; (ii) a fork-based process pool over the host cores this job may use.
+    The port is oracle.search_faithful — the reference's scipy/numpy call
+    sequence (bm25_native.py:147-158, 204-214)."""
+    from oracle import oracle  # the checker / CPU baseline (test infrastructure)
+    Q = queries.shape[0]
+    nq = min(args.cpu_queries, Q)
+    rng = np.random.default_rng(20240601)
+    sample = queries[np.sort(rng.choice(Q, size=nq, replace=False))]
+    aff = len(os.sched_getaffinity(0))
+    procs = args.cpu_procs
+    if procs <= 0:
+        procs = aff
+        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+            procs = min(procs, int(os.environ["OMP_NUM_THREADS"]))
+    procs = max(1, min(procs, nq))
+    m = oracle.faithful_matrix(n_docs, indptr, indices, data)
+    log(f"[rank 0] CPU baseline: {nq} sampled queries, 1 process ...")
+    t0 = time.perf_counter()
+    d1, s1 = oracle.search_faithful_m(m, sample, k)
+    t1 = time.perf_counter() - t0
+    log(f"[rank 0] CPU baseline: {nq} sampled queries, pool of {procs} processes ...")
+    d2, s2, t2 = oracle.search_faithful_pool(m, sample, k, procs)
+    if not np.array_equal(s1.view(np.uint32), s2.view(np.uint32)):
+        raise RuntimeError("CPU baseline legs disagree")
+    return {"value": round(nq / t2, 3), "unit": "queries/s", "cores": procs, "kind": "port",
+            "sample": f"{nq} queries drawn (seed 20240601) from the {Q}-query bench batch, same "
+                      f"index, k={k}; leg (ii): fork pool of {procs} processes, batch split "
+                      f"evenly; {t2:.2f} s; host {cpu_model()}, os.cpu_count()={os.cpu_count()}, "
+                      f"affinity {aff} cpus",
+            "single_core": {"value": round(nq / t1, 3), "unit": "queries/s", "cores": 1,
+                            "seconds": round(t1, 2)},
+            "batch_s_extrapolated": {"single_core": round(t1 / nq * Q, 1),
+                                     "pool": round(t2 / nq * Q, 1),
+                                     "note": f"EXTRAPOLATION: sample time x {Q}/{nq}"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--cpu-queries", type=int, default=-1,
-                    help="CPU baseline sample size (default: 16 for c3, 64 for c2; 0 = skip)")
+    ap.add_argument("--cpu-queries", type=int, default=64,
+                    help="CPU baseline: seeded query sample size (0 = skip)")
+    ap.add_argument("--cpu-procs", type=int, default=-1,
+                    help="CPU baseline pool leg: worker processes (default: the affinity "
+                         "mask's cores, capped at OMP_NUM_THREADS when that is set)")
+    ap.add_argument("--e2e-batches", type=int, default=20,
+                    help="host-buffer searches (H2D queries -> D2H results) timed for the "
+                         "end-to-end median")
     ap.add_argument("--threads", type=int, default=16, help="host threads for index generation")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--backend", default="nccl",
@@ -99,6 +147,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    cfg = synth.CONFIGS[args.config]
+    lo, hi = synth.shard_bounds(cfg.n_docs, world, rank)
+    t0 = time.time()
+    indptr, indices, data = synth.make_index(cfg, lo, hi, threads=args.threads)
+    log(f"[rank {rank}] shard docs [{lo},{hi}) nnz={int(indptr[-1])} generated in "
+        f"{time.time() - t0:.1f}s")
+    queries = synth.make_queries(cfg)
+
+    # CPU baseline first (rank 0 at N=1): its process pool forks before this
+    # process touches the GPU
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_queries > 0:
+        cpu = cpu_baseline(args, hi - lo, indptr, indices, data, queries, cfg.k)
+
     dist = None
     local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
@@ -110,18 +172,10 @@ def main():
             dist.init_process_group(args.backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    cfg = synth.CONFIGS[args.config]
-    lo, hi = synth.shard_bounds(cfg.n_docs, world, rank)
-    t0 = time.time()
-    indptr, indices, data = synth.make_index(cfg, lo, hi, threads=args.threads)
-    log(f"[rank {rank}] shard docs [{lo},{hi}) nnz={int(indptr[-1])} generated in "
-        f"{time.time() - t0:.1f}s")
     t0 = time.time()
     index = GpuIndex(indptr, indices, data, hi - lo, device=local, doc_offset=lo)
     info = index.info()
     log(f"[rank {rank}] index on cuda:{local} in {time.time() - t0:.1f}s: {info}")
-    queries = synth.make_queries(cfg)
     Q, T, k = queries.shape[0], queries.shape[1], cfg.k
     dq = torch.from_numpy(queries).to(dev)
     d_docs = torch.empty((Q, k), dtype=torch.int32, device=dev)
@@ -146,14 +200,34 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t_start = time.perf_counter()
+    evs[0].record(stream)
     for i in range(args.steps):
         step()
+        evs[i + 1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     prof = index.profile_read()
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    # end-to-end (N=1): the host-buffer entry point bm25_search — H2D of the
+    # query batch, the search, D2H of the [Q, k] results — timed per call
+    e2e = None
+    if world == 1 and args.e2e_batches > 0:
+        for _ in range(3):
+            index.search(queries, k)
+        ts = []
+        for _ in range(args.e2e_batches):
+            t0 = time.perf_counter()
+            index.search(queries, k)
+            ts.append(1000.0 * (time.perf_counter() - t0))
+        e2e = {"median_ms": round(float(np.median(ts)), 4), "min_ms": round(min(ts), 4),
+               "queries_per_s": round(Q / (float(np.median(ts)) * 1e-3), 1),
+               "batches": args.e2e_batches,
+               "what": "bm25_search host buffers: H2D queries -> search -> D2H docs+scores, "
+                       "host clock around the synchronous call"}
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -168,22 +242,6 @@ def main():
     shift = int(np.log2(info["tile_docs"]))
     traffic = load_traffic(args.traffic, args.config, shift) if world == 1 else None
 
-    cpu = None
-    if rank == 0 and world == 1:
-        nq = args.cpu_queries if args.cpu_queries >= 0 else (16 if args.config == "c3" else 64)
-        if nq > 0:
-            from oracle import oracle  # the checker / CPU baseline (test infrastructure)
-            sample = queries[:nq]
-            log(f"[rank 0] CPU baseline: bm25_native call sequence on {nq} queries ...")
-            t0 = time.perf_counter()
-            oracle.search_faithful(hi - lo, indptr, indices, data, sample, k)
-            dt = time.perf_counter() - t0
-            cpu = {"value": round(nq / dt, 3), "unit": "queries/s", "cores": 1, "kind": "port",
-                   "sample": f"first {nq} of the {Q} bench queries, same index, k={k}, "
-                             f"single process (scipy csc fancy-index + sum + argpartition, "
-                             f"bm25_native.py:149-158); {dt:.1f} s on {cpu_model()}, "
-                             f"host has {os.cpu_count()} logical cpus"}
-
     if rank == 0:
         out = {
             "metric": "queries/sec + achieved HBM GB/s, 10M-doc CSC index, batch=1024, k=100"
@@ -194,6 +252,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step_median": round(float(np.median(step_ms)), 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -220,6 +279,7 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
             },
             "cpu_baseline": cpu,
+            "e2e": e2e,
         }
         print(json.dumps(out), flush=True)
     index.close()

@@ -39,7 +39,9 @@ enum {
   BM25_OK = 0,
   BM25_EINVAL = 1, /* bad argument (bad shape, token id >= n_terms, k > n_docs ...) */
   BM25_EHIP = 2,   /* HIP runtime failure, or no usable GPU */
-  BM25_ERCCL = 3,  /* RCCL failure (sharded handles) */
+  /* 3 is unused: the one-process sharded handle moves its keys and lists with
+   * peer copies, and the multi-process path's collectives run in the caller
+   * (torch.distributed over RCCL, bm25mi.dist), not in this library */
   BM25_ENOMEM = 4  /* device or host allocation failed */
 };
 
@@ -107,6 +109,32 @@ int bm25_search_device(bm25_index* idx, const int32_t* d_queries, int64_t Q,
                        void* stream);
 
 /*
+ * GPU index build: (doc, term, tf) triples + document lengths -> the CSC
+ * score matrix (term-major, doc ids ascending per term = what
+ * bm25_index_create and the bm25s on-disk format hold).
+ * Replaces: the scoring half of the bm25s writer that produced the
+ *           reference's index (animal_index_bm25/*, params.index.json:1-11,
+ *           bm25_test.py:19-38; method 0) and BM25.fit's matrix
+ *           (bm25.py:30-121; method 1).
+ *   docs/terms [n] int32, tfs [n] f32 (> 0), any order, one triple per
+ *   (doc, term); doc_len [n_docs] int32; avgdl = the mean document length
+ *   (bm25.py:62 / bm25s); idf [n_terms] f32 or NULL (computed on the device:
+ *   ln(1 + (N - df + 0.5) / (df + 0.5)), df = triples per term);
+ *   method 0 = lucene: idf * tf / (tf + k1 * (1 - b + b * dl / avgdl)),
+ *   method 1 = bm25.py: idf * tf * (k1 + 1) / (tf + k1 * (1 - b + b * dl / avgdl)).
+ *   Outputs (host): out_indptr [n_terms+1] int64, out_indices [n] int32,
+ *   out_data [n] f32, out_data64 [n] f64 or NULL (method 1: the float64
+ *   bm25_matrix entries).  Operation order and precision follow the code each
+ *   method stands in for (bm25mi_build.hip), so the values are bit-identical.
+ * Errors: EINVAL for ids out of range, tf <= 0, duplicate (doc, term).
+ */
+int bm25_build_scores(int device, int64_t n_docs, int64_t n_terms, int64_t n_triples,
+                      const int32_t* docs, const int32_t* terms, const float* tfs,
+                      const int32_t* doc_len, double avgdl, double k1, double b, int method,
+                      const float* idf, int64_t* out_indptr, int32_t* out_indices,
+                      float* out_data, double* out_data64);
+
+/*
  * Dense per-document scores of one query (all n_docs fp32 sums, query-term
  * order, zero for untouched documents), host buffers.
  * Replaces: the dense gather+sum of the MAX graph (gpu_bm25/common.py:64-74)
@@ -167,10 +195,14 @@ int bm25_search_finish_device(bm25_index* idx, const int32_t* d_queries, int64_t
  *   bm25_sharded_create: same CSC arguments as bm25_index_create; documents
  *     are split into n_dev contiguous, 2048-doc-aligned ranges, shard s on
  *     devices[s] (a device may be listed more than once).
- *   bm25_sharded_search: same contract as bm25_search; each shard searches on
- *     its own stream, the per-shard [Q, k] lists are copied to devices[0]
- *     (peer copies) and merged there; the result equals a single-index search.
- *     Errors as bm25_search, plus EINVAL when k exceeds a shard's documents.
+ *   bm25_sharded_search: same contract as bm25_search; the global-threshold
+ *     protocol of the *_device calls above with peer copies (xGMI) in place of
+ *     the all-gathers: every shard samples on its own stream, every shard's
+ *     keys are copied to every device, every shard computes the world's theta
+ *     and lists its keys >= theta, and the [Q, k] lists are copied to
+ *     devices[0] and merged there; the result equals a single-index search.
+ *     Errors as bm25_search (k may exceed a shard's documents: its list is
+ *     padded).
  *   bm25_sharded_info: shard count and [lo, hi) doc ranges (arrays of n_dev).
  */
 typedef struct bm25_sharded bm25_sharded;

@@ -14,7 +14,7 @@ import re
 
 from .build import LIB
 
-BM25_OK, BM25_EINVAL, BM25_EHIP, BM25_ERCCL, BM25_ENOMEM = 0, 1, 2, 3, 4
+BM25_OK, BM25_EINVAL, BM25_EHIP, BM25_ENOMEM = 0, 1, 2, 4  # 3: unused (no RCCL inside the library)
 HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                       "include", "bm25mi.h")
 

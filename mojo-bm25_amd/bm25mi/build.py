@@ -18,8 +18,7 @@ REPO = os.path.dirname(os.path.dirname(PKG_DIR))
 LIB = os.environ.get("BM25MI_LIB") or os.path.join(PKG_DIR, "libbm25mi.so")
 SYNTH_LIB = os.path.join(PKG_DIR, "libbm25synth.so")
 
-HIP_SOURCES = ["bm25mi_kernels.hip", "bm25mi_capi.cpp"]
-HIP_DEPS = HIP_SOURCES + ["bm25mi_internal.h"]
+HIP_SOURCES = ["bm25mi_kernels.hip", "bm25mi_build.hip", "bm25mi_capi.cpp"]
 ARCH = os.environ.get("BM25_OFFLOAD_ARCH", "gfx950")
 
 
@@ -38,13 +37,27 @@ def _run(cmd, verbose):
 
 def build(force: bool = False, verbose: bool = False) -> None:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    deps = [os.path.join(CSRC, s) for s in HIP_DEPS] + [os.path.join(REPO, "include", "bm25mi.h")]
+    hdrs = [os.path.join(CSRC, "bm25mi_internal.h"), os.path.join(REPO, "include", "bm25mi.h")]
     lib = os.path.join(PKG_DIR, "libbm25mi.so")
-    if force or _stale(lib, deps):
+    objdir = os.path.join(PKG_DIR, "_obj")
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
+             "-Wno-unused-value"]
+    objs, jobs = [], []
+    for src in HIP_SOURCES:
+        o = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        objs.append(o)
+        if force or _stale(o, [os.path.join(CSRC, src)] + hdrs):
+            jobs.append([hipcc] + flags + ["-c", "-o", o + ".tmp", os.path.join(CSRC, src)])
+    if jobs:  # one hipcc per translation unit, in parallel
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(len(jobs)) as ex:
+            list(ex.map(lambda c: _run(c, verbose), jobs))
+        for c in jobs:
+            os.replace(c[-2], c[-2][:-4])
+    if force or jobs or _stale(lib, objs):
         tmp = lib + ".tmp"
-        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wno-unused-result", "-Wno-unused-value", "-o", tmp]
-             + [os.path.join(CSRC, s) for s in HIP_SOURCES], verbose)
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, verbose)
         os.replace(tmp, lib)
     sdeps = [os.path.join(CSRC, "synth.cpp")]
     if force or _stale(SYNTH_LIB, sdeps):

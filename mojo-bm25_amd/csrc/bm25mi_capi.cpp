@@ -231,11 +231,12 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
 }
 
 // Counters of the last search (caller holds h->mu); the search may run on a
-// caller's stream, so synchronise the device.
+// caller's stream: wait for its end event (ws_done), not for the device.
 void read_counters(bm25_index* h, int32_t (&cnt)[4]) {
   if (!h->ws.counters) return;
-  hipDeviceSynchronize();
-  hipMemcpy(cnt, h->ws.counters, sizeof cnt, hipMemcpyDeviceToHost);
+  if (h->ws_done) hipEventSynchronize(h->ws_done);
+  hipMemcpyAsync(cnt, h->ws.counters, sizeof cnt, hipMemcpyDeviceToHost, h->stream);
+  hipStreamSynchronize(h->stream);
 }
 
 // shard = true: the index is one doc shard of a larger collection, whose
@@ -508,6 +509,85 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   return BM25_OK;
 }
 
+int bm25_build_scores(int device, int64_t n_docs, int64_t n_terms, int64_t n_triples,
+                      const int32_t* docs, const int32_t* terms, const float* tfs,
+                      const int32_t* doc_len, double avgdl, double k1, double b, int method,
+                      const float* idf, int64_t* out_indptr, int32_t* out_indices,
+                      float* out_data, double* out_data64) {
+  if (n_docs < 0 || n_terms < 0 || n_triples < 0)
+    return fail(BM25_EINVAL, "negative size (n_docs=%lld n_terms=%lld n=%lld)", (long long)n_docs,
+                (long long)n_terms, (long long)n_triples);
+  if (n_docs > INT32_MAX || n_terms > INT32_MAX || n_triples > INT32_MAX)
+    return fail(BM25_EINVAL, "sizes above int32 are built per shard");
+  if (method != kLucene && method != kBm25Py) return fail(BM25_EINVAL, "unknown method %d", method);
+  if (!out_indptr || (n_triples > 0 && (!docs || !terms || !tfs || !doc_len || !out_indices ||
+                                         !out_data)))
+    return fail(BM25_EINVAL, "NULL argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(BM25_EHIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(BM25_EINVAL, "device %d out of range (%d visible)", device, ndev);
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+  const size_t n = (size_t)std::max<int64_t>(n_triples, 1);
+  int32_t *d_docs = nullptr, *d_terms = nullptr, *d_dl = nullptr, *d_ix = nullptr, *d_err = nullptr;
+  float *d_tf = nullptr, *d_idf = nullptr, *d_dt = nullptr;
+  double* d_dt64 = nullptr;
+  int64_t* d_ip = nullptr;
+  hipStream_t st = nullptr;
+  auto cleanup = [&](int rc) {
+    if (st) hipStreamSynchronize(st);
+    for (void* p : {(void*)d_docs, (void*)d_terms, (void*)d_dl, (void*)d_ix, (void*)d_err,
+                    (void*)d_tf, (void*)d_idf, (void*)d_dt, (void*)d_dt64, (void*)d_ip})
+      hipFree(p);
+    if (st) hipStreamDestroy(st);
+    return rc;
+  };
+  hipError_t e;
+#define TRYB(expr, what)                                    \
+  do {                                                      \
+    e = (expr);                                             \
+    if (e != hipSuccess) return cleanup(hip_fail(e, what)); \
+  } while (0)
+  TRYB(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  TRYB(hipMalloc(&d_docs, sizeof(int32_t) * n), "hipMalloc(docs)");
+  TRYB(hipMalloc(&d_terms, sizeof(int32_t) * n), "hipMalloc(terms)");
+  TRYB(hipMalloc(&d_tf, sizeof(float) * n), "hipMalloc(tf)");
+  TRYB(hipMalloc(&d_dl, sizeof(int32_t) * std::max<int64_t>(n_docs, 1)), "hipMalloc(doc_len)");
+  TRYB(hipMalloc(&d_ix, sizeof(int32_t) * n), "hipMalloc(indices)");
+  TRYB(hipMalloc(&d_dt, sizeof(float) * n), "hipMalloc(data)");
+  TRYB(hipMalloc(&d_ip, sizeof(int64_t) * (n_terms + 1)), "hipMalloc(indptr)");
+  TRYB(hipMalloc(&d_err, sizeof(int32_t)), "hipMalloc(err)");
+  if (out_data64) TRYB(hipMalloc(&d_dt64, sizeof(double) * n), "hipMalloc(data64)");
+  if (idf) {
+    TRYB(hipMalloc(&d_idf, sizeof(float) * std::max<int64_t>(n_terms, 1)), "hipMalloc(idf)");
+    TRYB(hipMemcpyAsync(d_idf, idf, sizeof(float) * n_terms, hipMemcpyHostToDevice, st), "H2D idf");
+  }
+  TRYB(hipMemsetAsync(d_err, 0, sizeof(int32_t), st), "hipMemset");
+  if (n_triples > 0) {
+    TRYB(hipMemcpyAsync(d_docs, docs, sizeof(int32_t) * n_triples, hipMemcpyHostToDevice, st), "H2D docs");
+    TRYB(hipMemcpyAsync(d_terms, terms, sizeof(int32_t) * n_triples, hipMemcpyHostToDevice, st), "H2D terms");
+    TRYB(hipMemcpyAsync(d_tf, tfs, sizeof(float) * n_triples, hipMemcpyHostToDevice, st), "H2D tf");
+    TRYB(hipMemcpyAsync(d_dl, doc_len, sizeof(int32_t) * n_docs, hipMemcpyHostToDevice, st), "H2D doc_len");
+  }
+  TRYB(build_scores(n_docs, n_terms, n_triples, d_docs, d_terms, d_tf, d_dl, avgdl, k1, b, method,
+                    d_idf, d_ip, d_ix, d_dt, d_dt64, d_err, st), "build_scores");
+  int32_t herr = 0;
+  TRYB(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, st), "D2H err");
+  TRYB(hipStreamSynchronize(st), "build sync");
+  if (herr & 1) return cleanup(fail(BM25_EINVAL, "doc or term id out of range"));
+  if (herr & 2) return cleanup(fail(BM25_EINVAL, "term frequencies must be positive and finite"));
+  if (herr & 4) return cleanup(fail(BM25_EINVAL, "duplicate (doc, term) triple"));
+  TRYB(hipMemcpyAsync(out_indptr, d_ip, sizeof(int64_t) * (n_terms + 1), hipMemcpyDeviceToHost, st), "D2H indptr");
+  if (n_triples > 0) {
+    TRYB(hipMemcpyAsync(out_indices, d_ix, sizeof(int32_t) * n_triples, hipMemcpyDeviceToHost, st), "D2H indices");
+    TRYB(hipMemcpyAsync(out_data, d_dt, sizeof(float) * n_triples, hipMemcpyDeviceToHost, st), "D2H data");
+    if (out_data64)
+      TRYB(hipMemcpyAsync(out_data64, d_dt64, sizeof(double) * n_triples, hipMemcpyDeviceToHost, st), "D2H data64");
+  }
+  TRYB(hipStreamSynchronize(st), "build sync");
+#undef TRYB
+  return cleanup(BM25_OK);
+}
+
 int bm25_scores_dense(bm25_index* h, const int32_t* query, int64_t T, float* out_scores) {
   if (!h) return fail(BM25_EINVAL, "NULL index");
   if (T < 0) return fail(BM25_EINVAL, "negative query length");
@@ -591,16 +671,30 @@ int bm25_search_stats(bm25_index* h, int64_t* rescored_tiles, int64_t* fallback_
 // ---------------------------------------------------------------------------
 // Doc-sharded index over several devices of one process:
 // shard s owns the tile-aligned doc range [lo_s, hi_s) as an ordinary index
-// (doc_offset = lo_s) on devices[s]; a search runs every shard on its own
-// stream, copies the per-shard [Q, k] lists to shard 0's device (peer copies
-// ordered by events) and merges them there with merge_lists_kernel — the same
-// (score desc, doc asc) rule, so the result equals a single-index search.
+// (doc_offset = lo_s) on devices[s].  A search is the global-threshold
+// protocol of the multi-process path (bm25mi.dist.sharded_search) with peer
+// copies over xGMI in place of the collectives:
+//   1. every shard samples on its own stream -> keys_s [Q][S];
+//   2. every shard's keys are copied into every shard's all_keys [W][Q][S]
+//      (peer copies on the destination's stream, after the source's event);
+//   3. every shard: theta = the k-th best key of the whole sample, then its
+//      keys >= theta as a padded [Q, k] list (global doc ids);
+//   4. the lists are copied to shard 0's device and merged there with the
+//      same (score desc, doc asc) rule, so the result equals a single-index
+//      search.
+// One process owns every device here, so no RCCL communicator is involved
+// (the multi-process path runs its all-gathers over RCCL).
 // ---------------------------------------------------------------------------
 struct bm25_sharded {
   std::vector<bm25_index*> shards;
   std::vector<int64_t> lo, hi;
-  std::vector<hipEvent_t> done;  // per shard: its search finished
-  int64_t n_docs = 0, n_terms = 0;
+  std::vector<hipEvent_t> sampled;  // per shard: its sample keys are written
+  std::vector<hipEvent_t> keyed;    // per shard: its all_keys copies landed
+  std::vector<hipEvent_t> done;     // per shard: its [Q, k] list is written
+  std::vector<uint64_t*> keys;      // per shard (own device): [Q][S]
+  std::vector<uint64_t*> all_keys;  // per shard (own device): [W][Q][S]
+  int64_t cap_keys = 0;
+  int64_t n_docs = 0, n_terms = 0, shard_docs_max = 0;
   int32_t* g_docs = nullptr;     // [W][Q][k] on shard 0's device
   float* g_scores = nullptr;
   int32_t* m_docs = nullptr;     // [Q][k]
@@ -623,7 +717,11 @@ int sharded_free(bm25_sharded* s) {
   for (size_t i = 0; i < s->shards.size(); ++i) {
     if (!s->shards[i]) continue;
     hipSetDevice(s->shards[i]->ix.device);
-    if (i < s->done.size() && s->done[i]) hipEventDestroy(s->done[i]);
+    hipStreamSynchronize(s->shards[i]->stream);
+    for (auto* v : {&s->sampled, &s->keyed, &s->done})
+      if (i < v->size() && (*v)[i]) hipEventDestroy((*v)[i]);
+    if (i < s->keys.size()) hipFree(s->keys[i]);
+    if (i < s->all_keys.size()) hipFree(s->all_keys[i]);
     bm25_index_destroy(s->shards[i]);
   }
   delete s;
@@ -695,13 +793,18 @@ int bm25_sharded_create(int n_dev, const int* devices, int64_t n_docs, int64_t n
     s->shards.push_back(h);
     s->lo.push_back(lo);
     s->hi.push_back(hi);
-    hipEvent_t ev = nullptr;
+    s->keys.push_back(nullptr);
+    s->all_keys.push_back(nullptr);
+    s->shard_docs_max = std::max(s->shard_docs_max, hi - lo);
     hipSetDevice(devices[r]);
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-      sharded_free(s);
-      return fail(BM25_EHIP, "hipEventCreate");
+    for (auto* v : {&s->sampled, &s->keyed, &s->done}) {
+      hipEvent_t ev = nullptr;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        sharded_free(s);
+        return fail(BM25_EHIP, "hipEventCreate");
+      }
+      v->push_back(ev);
     }
-    s->done.push_back(ev);
   }
   *out = s;
   return BM25_OK;
@@ -751,17 +854,65 @@ int bm25_sharded_search(bm25_sharded* s, const int32_t* queries, int64_t Q, int6
     HIP_TRY(hipMalloc(&s->m_scores, sizeof(float) * out), "hipMalloc(merged)");
     s->cap_m = out;
   }
-  // every shard: H2D queries + search on its own stream, then an event
+  // sample width: the same on every shard (bm25_sample_width's rule)
+  int64_t S = 0;
+  int rc = bm25_sample_width(h0, s->shard_docs_max, (int32_t)W, k, &S);
+  if (rc) return rc;
+  if (Q * S > s->cap_keys) {
+    for (int64_t r = 0; r < W; ++r) {
+      HIP_TRY(hipSetDevice(s->shards[r]->ix.device), "hipSetDevice");
+      hipStreamSynchronize(s->shards[r]->stream);
+      hipFree(s->keys[r]);
+      hipFree(s->all_keys[r]);
+      s->keys[r] = s->all_keys[r] = nullptr;
+      HIP_TRY(hipMalloc(&s->keys[r], sizeof(uint64_t) * Q * S), "hipMalloc(sample keys)");
+      HIP_TRY(hipMalloc(&s->all_keys[r], sizeof(uint64_t) * W * Q * S), "hipMalloc(all keys)");
+    }
+    s->cap_keys = Q * S;
+  }
+  // 1. every shard: H2D queries + its sample keys, on its own stream
   for (int64_t r = 0; r < W; ++r) {
     bm25_index* h = s->shards[r];
-    std::lock_guard<std::mutex> lh(h->mu);
     HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
-    int rc = ensure_io(h, Q * T, out);
-    if (rc) return rc;
-    if (Q * T > 0)
-      HIP_TRY(hipMemcpyAsync(h->d_q, queries, sizeof(int32_t) * Q * T, hipMemcpyHostToDevice,
-                             h->stream), "H2D queries");
-    rc = run_search(h, h->d_q, Q, T, k, h->d_docs, h->d_scores, h->stream);
+    {
+      std::lock_guard<std::mutex> lh(h->mu);
+      rc = ensure_io(h, Q * T, out);
+      if (rc) return rc;
+      if (Q * T > 0)
+        HIP_TRY(hipMemcpyAsync(h->d_q, queries, sizeof(int32_t) * Q * T, hipMemcpyHostToDevice,
+                               h->stream), "H2D queries");
+    }
+    if (S > 0) {
+      rc = bm25_search_sample_device(h, h->d_q, Q, T, k, (int32_t)W, s->shard_docs_max,
+                                     s->keys[r], h->stream);
+      if (rc) return rc;
+    }
+    HIP_TRY(hipEventRecord(s->sampled[r], h->stream), "hipEventRecord");
+  }
+  // 2. every shard's keys into every shard's all_keys (destination stream)
+  if (S > 0) {
+    for (int64_t d = 0; d < W; ++d) {
+      bm25_index* hd = s->shards[d];
+      HIP_TRY(hipSetDevice(hd->ix.device), "hipSetDevice");
+      for (int64_t r = 0; r < W; ++r) {
+        bm25_index* hr = s->shards[r];
+        HIP_TRY(hipStreamWaitEvent(hd->stream, s->sampled[r], 0), "hipStreamWaitEvent");
+        HIP_TRY(hipMemcpyPeerAsync(s->all_keys[d] + r * Q * S, hd->ix.device, s->keys[r],
+                                   hr->ix.device, sizeof(uint64_t) * Q * S, hd->stream),
+                "peer copy (sample keys)");
+      }
+      HIP_TRY(hipEventRecord(s->keyed[d], hd->stream), "hipEventRecord");
+    }
+  }
+  // 3. every shard: global theta, REST, its padded [Q, k] list (a shard's
+  // keys buffer is rewritten only by the next search, and this one waits for
+  // every keyed[*] event before it returns)
+  for (int64_t r = 0; r < W; ++r) {
+    bm25_index* h = s->shards[r];
+    HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+    rc = bm25_search_finish_device(h, h->d_q, Q, T, k, (int32_t)W, s->shard_docs_max,
+                                   S > 0 ? s->all_keys[r] : nullptr, h->d_docs, h->d_scores,
+                                   h->stream);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(s->done[r], h->stream), "hipEventRecord");
   }
@@ -782,6 +933,11 @@ int bm25_sharded_search(bm25_sharded* s, const int32_t* queries, int64_t Q, int6
   HIP_TRY(hipMemcpyAsync(out_scores, s->m_scores, sizeof(float) * out, hipMemcpyDeviceToHost,
                          h0->stream), "D2H scores");
   HIP_TRY(hipStreamSynchronize(h0->stream), "sharded search sync");
+  // every shard's stream has drained its copies of the others' keys
+  for (int64_t r = 0; r < W; ++r) {
+    HIP_TRY(hipSetDevice(s->shards[r]->ix.device), "hipSetDevice");
+    HIP_TRY(hipEventSynchronize(s->keyed[r]), "hipEventSynchronize");
+  }
   return BM25_OK;
 }
 

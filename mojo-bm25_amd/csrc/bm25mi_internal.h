@@ -134,4 +134,16 @@ hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores,
 // Tile shifts with compiled kernels.
 bool tile_shift_supported(int s);
 
+// GPU index build (bm25mi_build.hip): scoring rules of bm25_build_scores.
+enum { kLucene = 0, kBm25Py = 1 };
+// (doc, term, tf) triples + document lengths -> CSC indptr [n_terms+1] (i64),
+// indices/data [n] (+ f64 data when d_data64 != null), all on the device;
+// d_err |= 1 (id out of range), 2 (tf not positive finite), 4 (duplicate
+// (doc, term)).  Synchronises `stream` before returning.
+hipError_t build_scores(int64_t n_docs, int64_t n_terms, int64_t n, const int32_t* d_docs,
+                        const int32_t* d_terms, const float* d_tfs, const int32_t* d_doc_len,
+                        double avgdl, double k1, double b, int method, const float* d_idf,
+                        int64_t* d_indptr, int32_t* d_indices, float* d_data, double* d_data64,
+                        int32_t* d_err, hipStream_t stream);
+
 }  // namespace bm25mi

@@ -27,6 +27,8 @@
 // score vector, with untouched documents scoring 0.
 #include "bm25mi_internal.h"
 
+#include <map>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -2061,15 +2063,26 @@ SampleGeom sample_geom(int64_t ntiles, int k, int W) {
   return SampleGeom{1, 0, 0, 1};
 }
 
+// Every resident workgroup slot of the current device (a multiple of 8, one
+// per XCD round), cached per (kernel, device).
 template <int S, int PH, class K>
 static int persistent_grid(K kernel) {
-  int dev = 0, cus = 0, occ = 0;
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  int dev = 0;
   hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair((const void*)kernel, dev);
+  const auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int cus = 0, occ = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 64 * kWaves, 0);
   const char* e = getenv("BM25_WG_PER_CU");
   if (e) occ = atoi(e);
-  return ((cus * (occ > 0 ? occ : 1) + 7) / 8) * 8;  // every resident slot, a multiple of 8
+  const int g = ((cus * (occ > 0 ? occ : 1) + 7) / 8) * 8;
+  cache[key] = g;
+  return g;
 }
 
 // The pipelined kernel serves queries of 1..64 terms (BM25_NO_PIPE=1 forces
@@ -2114,7 +2127,7 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
       return;
     }
   }
-  static const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH, QMAP, DIAG, SM>);
+  const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH, QMAP, DIAG, SM>);
   hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrInts, st);
   uint64_t* stamps = nullptr;
   if (DIAG & 32) {
@@ -2168,7 +2181,7 @@ static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const S
       return;
     }
   }
-  static const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM>);
+  const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM>);
   hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrInts, st);
   // REST skips the sample tiles whose best key is below theta (m = 1 samples
   // in groups of one band: ws.cand holds this shard's sample keys)
@@ -2206,7 +2219,7 @@ static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const S
       launch_pipe<S, PH, false, 32>(ix, q, T, sg, ws, st);
     return;
   }
-  static const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
+  const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
   hipLaunchKernelGGL((score_wave_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0, st,
                      args_of(ix), q, (int32_t)T, sg, ws.theta, sg.cand_out, ws.list, ws.list_cnt,
                      ws.list_cap);
@@ -2301,7 +2314,11 @@ static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
 hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                          const SampleGeom& g, uint64_t* keys, const Workspace& ws,
                          hipStream_t stream) {
-  if (Q == 0 || ix.ntiles == 0 || g.P == 1) return hipSuccess;
+  if (Q == 0 || g.P == 1) return hipSuccess;
+  if (ix.ntiles == 0) {  // an empty doc shard contributes no keys
+    hipMemsetAsync(keys, 0, sizeof(uint64_t) * Q * g.S, stream);
+    return hipGetLastError();
+  }
 #define CALL(s) sample_s<s>(ix, d_queries, Q, T, g, keys, ws, stream)
   BM25_SHIFT_DISPATCH(CALL)
 #undef CALL

@@ -508,3 +508,27 @@ def test_global_theta_ties_across_shards(gpu, W):
         merge_topk_device(0, lists_d, lists_s, W, len(q), k, md, ms, st)
         torch.cuda.synchronize()
         _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)
+
+
+def test_sharded_index_global_theta_ties_and_small_shards(gpu):
+    """bm25_sharded_search runs the global-threshold protocol (every shard's
+    sample keys peer-copied to every device): tie groups cut by k that span
+    shards keep the smallest global ids; shards smaller than k pad their
+    lists; a one-tile collection split over more devices than tiles works."""
+    from bm25mi.index import ShardedIndex
+    rng = np.random.default_rng(77)
+    N, V = 700_000, 12
+    ip, ix, dt = _rand_index(rng, N, V, 300_000, coarse=True)
+    dt[ip[0]:ip[1]] = 1.0
+    q = np.array([[0, -1, -1], [0, 0, -1], [1, 2, 3], [4, 4, 5], [0, 6, 7], [8, 9, 10]],
+                 np.int32)
+    sh = ShardedIndex(ip, ix, dt, N, devices=[0, 0, 0])
+    for k in (100, 777):
+        _exact(sh.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+    sh.close()
+    for N, devs, k in ((3000, [0, 0], 2500), (1500, [0, 0, 0], 1500)):
+        ip, ix, dt = _rand_index(rng, N, 40, 4000)
+        qq = rng.integers(-1, 40, size=(9, 4)).astype(np.int32)
+        sh = ShardedIndex(ip, ix, dt, N, devices=devs)
+        _exact(sh.search(qq, k), oracle.search_c(N, ip, ix, dt, qq, k))
+        sh.close()
