@@ -121,7 +121,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c3")
+    ap.add_argument("--config", default="c3", help="c3 (headline), c2, c5 (100M docs: one GPU "
+                    "runs one rank's doc shard, see --c5-rank)")
+    ap.add_argument("--c5-rank", type=int, default=0,
+                    help="config 5 at N=1: which of the 8 doc shards of the 8-GPU job to run")
     ap.add_argument("--cpu-queries", type=int, default=64,
                     help="CPU baseline: seeded query sample size (0 = skip)")
     ap.add_argument("--cpu-procs", type=int, default=-1,
@@ -148,7 +151,13 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     cfg = synth.CONFIGS[args.config]
-    lo, hi = synth.shard_bounds(cfg.n_docs, world, rank)
+    # config 5 holds 6.4B postings: one GPU runs one of the 8 ranks' shards
+    # (800M postings, int64 global indptr cut per rank by the generator)
+    emul = 8 if (args.config == "c5" and world == 1) else 0
+    if emul:
+        lo, hi = synth.shard_bounds(cfg.n_docs, emul, args.c5_rank)
+    else:
+        lo, hi = synth.shard_bounds(cfg.n_docs, world, rank)
     t0 = time.time()
     indptr, indices, data = synth.make_index(cfg, lo, hi, threads=args.threads)
     log(f"[rank {rank}] shard docs [{lo},{hi}) nnz={int(indptr[-1])} generated in "
@@ -245,7 +254,9 @@ def main():
     if rank == 0:
         out = {
             "metric": "queries/sec + achieved HBM GB/s, 10M-doc CSC index, batch=1024, k=100"
-            if args.config == "c3" else f"queries/sec, {cfg.name}",
+            if args.config == "c3" else (f"queries/sec per rank, {cfg.name}, rank "
+                                         f"{args.c5_rank} of 8 (standalone shard search)"
+                                         if emul else f"queries/sec, {cfg.name}"),
             "value": round(qps, 2),
             "unit": "queries/s",
             "n_gpus": world,
@@ -259,7 +270,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded Zipf CSC index + df^0.75 queries, csrc/synth.cpp)",
             "config": {
-                "workload": f"{args.config}: {cfg.name}",
+                "workload": f"{args.config}: {cfg.name}" + (
+                    f"; one rank's doc shard [{lo}, {hi}) of the 8-GPU job" if emul else ""),
+                "segments": "sparse" if info.get("sparse") else "dense",
                 "n_docs": cfg.n_docs, "n_terms": cfg.n_terms, "nnz": int(indptr[-1]) if world == 1
                 else cfg.nnz, "batch": Q, "terms_per_query": T, "k": k,
                 "tile_docs": info["tile_docs"],

@@ -86,6 +86,14 @@ int bm25_index_info(const bm25_index* idx, int64_t* n_docs, int64_t* n_terms,
                     int64_t* device_bytes);
 
 /*
+ * Segment table of a built index: *sparse = 0 for the dense
+ * V x (n_tiles+1) table, 1 for per-term tile lists (chosen at create time:
+ * env BM25_SEGMENTS=dense|sparse, else dense unless it would exceed twice the
+ * posting arrays); *n_pairs = non-empty (term, tile) pairs held (sparse).
+ */
+int bm25_index_segments(const bm25_index* idx, int32_t* sparse, int64_t* n_pairs);
+
+/*
  * Batched top-k search, host buffers, synchronous.
  * Replaces: BM25v.search / get_scores / _compute_relevance_from_scores / _topk
  *           (bm25_native.py:76-158, 204-214).

@@ -1,10 +1,12 @@
 """Drop-in replacement of the reference's ``bm25`` module (dense BM25 model).
 
 Same class, constructor, attributes and methods as ``bm25.py:6-178`` of
-yuhuishi-convect/mojo-bm25.  ``fit`` builds the same dense document x term
-BM25 matrix on the host (bm25.py:30-121: Robertson idf + 1, ``(k1 + 1)``
-numerator, float64 as in the reference) and uploads its non-zeros as a CSC
-index to the MI355X; ``get_scores`` / ``get_top_n`` (bm25.py:124-178) then run
+yuhuishi-convect/mojo-bm25.  ``fit`` counts terms on the host (like the
+tokenisation) and builds the BM25 matrix on the MI355X with
+``bm25_build_scores`` (bm25.py:106-121: Robertson idf + 1, ``(k1 + 1)``
+numerator, the reference's float64 arithmetic and operation order), which
+returns the CSC index data and the float64 entries of the reference's dense
+``bm25_matrix``; ``get_scores`` / ``get_top_n`` (bm25.py:124-178) then run
 through libbm25mi's kernels (dense per-document scores / batched top-k).
 
 Numerics: the engine sums the query terms' scores in fp32 (the values cast
@@ -25,6 +27,7 @@ import numpy as np
 import scipy.sparse as sp
 
 from bm25mi.index import GpuIndex
+from bm25mi.scoring import build_scores
 
 MAX_TOP_K = 4096  # kMaxK of libbm25mi (bm25mi_internal.h)
 
@@ -77,34 +80,37 @@ class BM25:
             self.idf = {}
             self.tf = np.zeros((self.corpus_size, 0))
             return
-        self.tf = np.zeros((self.corpus_size, num_terms), dtype=np.float32)
-        doc_presence = np.zeros((self.corpus_size, num_terms), dtype=bool)
+        # (doc, term, tf) triples; the counting stays on the host like the
+        # tokenisation (bm25.py:76-86)
+        docs, terms, tfs = [], [], []
         for i, doc_tokens in enumerate(corpus):
             for term, count in Counter(doc_tokens).items():
-                term_id = self.term_to_id[term]
-                self.tf[i, term_id] = count
-                doc_presence[i, term_id] = True
-        doc_freq_counts = np.sum(doc_presence, axis=0)
+                docs.append(i)
+                terms.append(self.term_to_id[term])
+                tfs.append(count)
+        docs = np.asarray(docs, np.int32)
+        terms = np.asarray(terms, np.int32)
+        tfs = np.asarray(tfs, np.float32)
+        doc_freq_counts = np.bincount(terms, minlength=num_terms)
         self.doc_freqs = {self.vocabulary[j]: doc_freq_counts[j] for j in range(num_terms)}
         N = self.corpus_size
-        self.idf = {}
+        self.idf = {}  # bm25.py:95-103 (math.log, host: V values)
         for term in self.vocabulary:
             df = self.doc_freqs[term]
             if N - df + 0.5 > 0 and df + 0.5 > 0:
                 self.idf[term] = math.log((N - df + 0.5) / (df + 0.5) + 1)
             else:
                 self.idf[term] = 0.0
-        doc_len_np = np.array(self.doc_len, dtype=np.float32)
-        if self.avgdl == 0:
-            length_norm_factor = self.k1 * (1 - self.b)
-        else:
-            length_norm_factor = self.k1 * (1 - self.b + self.b * doc_len_np / self.avgdl)
-        denominator = self.tf + length_norm_factor[:, np.newaxis]
-        term_scores_matrix = (self.tf * (self.k1 + 1)) / denominator
         idf_vec = np.array([self.idf[term] for term in self.vocabulary], dtype=np.float32)
-        self.bm25_matrix = term_scores_matrix * idf_vec[np.newaxis, :]
-        self._gpu = GpuIndex.from_csc(sp.csc_matrix(self.bm25_matrix.astype(np.float32)),
-                                      device=self.device)
+        # the matrix (bm25.py:106-121) on the GPU: CSC f32 for the index plus
+        # the float64 entries of the reference's dense bm25_matrix
+        indptr, indices, data, data64 = build_scores(
+            docs, terms, tfs, np.asarray(self.doc_len, np.int32), num_terms, k1=self.k1, b=self.b,
+            method="bm25py", avgdl=self.avgdl, idf=idf_vec, device=self.device, want_f64=True)
+        shape = (self.corpus_size, num_terms)
+        self.tf = sp.csc_matrix((tfs, (docs, terms)), shape=shape).toarray()
+        self.bm25_matrix = sp.csc_matrix((data64, indices, indptr), shape=shape).toarray()
+        self._gpu = GpuIndex(indptr, indices, data, self.corpus_size, device=self.device)
 
     # --------------------------------------------------------------- scoring
     def _query_ids(self, query):

@@ -51,6 +51,7 @@ _SIGS = {
                            ctypes.POINTER(_P)], ctypes.c_int),
     "bm25_index_destroy": ([_P], ctypes.c_int),
     "bm25_index_info": ([_P, _PI64, _PI64, _PI64, _PI32, _PI64, _PI64], ctypes.c_int),
+    "bm25_index_segments": ([_P, _PI32, _PI64], ctypes.c_int),
     "bm25_search": ([_P, _P, _I64, _I64, _I32, _P, _P], ctypes.c_int),
     "bm25_search_device": ([_P, _P, _I64, _I64, _I32, _P, _P, _P], ctypes.c_int),
     "bm25_scores_dense": ([_P, _P, _I64, _P], ctypes.c_int),
@@ -68,6 +69,9 @@ _SIGS = {
     "bm25_search_sample_device": ([_P, _P, _I64, _I64, _I32, _I32, _I64, _P, _P], ctypes.c_int),
     "bm25_search_finish_device": ([_P, _P, _I64, _I64, _I32, _I32, _I64, _P, _P, _P, _P],
                                   ctypes.c_int),
+    "bm25_build_scores": ([ctypes.c_int, _I64, _I64, _I64, _P, _P, _P, _P, ctypes.c_double,
+                           ctypes.c_double, ctypes.c_double, ctypes.c_int, _P, _P, _P, _P, _P],
+                          ctypes.c_int),
 }
 for _name, (_args, _res) in _SIGS.items():
     _f = getattr(lib, _name)

@@ -15,7 +15,9 @@ A bm25s index directory — what ``retriever.save(dir)`` writes
 ``load_bm25s`` memory-maps the three arrays (``numpy.load(mmap_mode="r")``,
 never unpickling) and validates their shapes; ``open_index`` uploads them to a
 GPU (the device build rejects unsorted / out-of-range doc ids);
-``query_ids`` maps tokens to ids the way a caller of ``BM25v.search`` would.
+``query_ids`` maps tokens to ids the way a caller of ``BM25v.search`` would;
+``save_bm25s`` writes the same layout (e.g. from bm25mi.scoring's GPU build);
+bm25mi.shard.load_bm25s_shard reads one rank's doc shard of it.
 """
 from __future__ import annotations
 
@@ -94,6 +96,39 @@ def load_bm25s(path: str, mmap: bool = True) -> Bm25sIndex:
     if "num_docs" not in params:
         raise ValueError(f"{path}: params.index.json has no num_docs")
     return Bm25sIndex(ip, ix, dt, params, vocab, path)
+
+
+def save_bm25s(path: str, indptr, indices, data, num_docs: int,
+               vocab: Optional[Dict[str, int]] = None, params: Optional[dict] = None,
+               corpus: Optional[List[dict]] = None) -> None:
+    """Write a bm25s index directory (the layout ``load_bm25s`` reads:
+    ``.npy`` arrays without pickles, params/vocab JSON, optional corpus.jsonl
+    + corpus.mmindex.json byte offsets).  ``indptr`` keeps its integer width
+    (int64 once nnz passes 2^31)."""
+    os.makedirs(path, exist_ok=True)
+    ip = np.asarray(indptr)
+    if ip.dtype not in (np.int32, np.int64):
+        ip = ip.astype(np.int64)
+    for name, arr in (("indptr", ip), ("indices", np.asarray(indices, np.int32)),
+                      ("data", np.asarray(data, np.float32))):
+        np.save(os.path.join(path, f"{name}.csc.index.npy"), arr, allow_pickle=False)
+    prm = {"k1": 1.5, "b": 0.75, "delta": 0.5, "method": "lucene", "idf_method": "lucene",
+           "dtype": "float32", "int_dtype": "int64" if ip.dtype == np.int64 else "int32",
+           "num_docs": int(num_docs), "version": "0.2.12", "backend": "numpy"}
+    prm.update(params or {})
+    prm["num_docs"] = int(num_docs)
+    with open(os.path.join(path, "params.index.json"), "w") as f:
+        json.dump(prm, f, indent=4)
+    with open(os.path.join(path, "vocab.index.json"), "w", encoding="utf-8") as f:
+        json.dump(vocab or {}, f)
+    if corpus is not None:
+        offs = []
+        with open(os.path.join(path, "corpus.jsonl"), "wb") as f:
+            for doc in corpus:
+                offs.append(f.tell())
+                f.write((json.dumps(doc) + "\n").encode("utf-8"))
+        with open(os.path.join(path, "corpus.mmindex.json"), "w") as f:
+            json.dump(offs, f)
 
 
 def open_index(path: str, device: int = 0):

@@ -86,8 +86,12 @@ class GpuIndex:
         db = ctypes.c_int64()
         check(lib.bm25_index_info(self._h, *[ctypes.byref(v) for v in vals], ctypes.byref(td),
                                   ctypes.byref(nt), ctypes.byref(db)))
+        sp_ = ctypes.c_int32()
+        npairs = ctypes.c_int64()
+        check(lib.bm25_index_segments(self._h, ctypes.byref(sp_), ctypes.byref(npairs)))
         return {"n_docs": vals[0].value, "n_terms": vals[1].value, "nnz": vals[2].value,
-                "tile_docs": td.value, "n_tiles": nt.value, "device_bytes": db.value}
+                "tile_docs": td.value, "n_tiles": nt.value, "device_bytes": db.value,
+                "sparse": bool(sp_.value), "n_pairs": npairs.value}
 
     # ------------------------------------------------------------------
     def search(self, queries: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:

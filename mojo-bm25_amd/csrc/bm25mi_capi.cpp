@@ -92,6 +92,7 @@ void free_ws(Workspace& ws) {
   hipFree(ws.queue);
   hipFree(ws.counters);
   hipFree(ws.wctr);
+  hipFree(ws.seg);
   ws = Workspace{};
 }
 
@@ -126,6 +127,8 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
   HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * 4), "hipMemset(counters)");
   HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrInts), "hipMalloc(wctr)");
+  ws.cap_seg = seg_entries(h->ix, q);
+  if (ws.cap_seg > 0) HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * ws.cap_seg), "hipMalloc(seg)");
   ws.list_cap = C;
   ws.cap_q = q;
   ws.cap_k = kk;
@@ -326,16 +329,27 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     if (e != hipSuccess) return cleanup(hip_fail(e, what));       \
   } while (0)
   TRYC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+  // segment table form (DevIndex): BM25_SEGMENTS=dense|sparse; by default the
+  // dense V x (ntiles+1) table unless it would outgrow twice the posting
+  // arrays (6 B per posting) — then the O(pairs) tile lists
   const int64_t rel_elems = n_terms * (ntiles + 1);
+  {
+    const char* m = getenv("BM25_SEGMENTS");
+    if (m && !strcmp(m, "sparse")) ix.sparse = true;
+    else if (m && !strcmp(m, "dense")) ix.sparse = false;
+    else ix.sparse = rel_elems * 4 > 2 * 6 * std::max<int64_t>(nnz, 1);
+  }
   TRYC(hipMalloc(&ix.indptr, sizeof(int64_t) * (n_terms + 1)), "hipMalloc(indptr)");
-  TRYC(hipMalloc(&ix.rel, sizeof(uint32_t) * std::max<int64_t>(rel_elems, 1)), "hipMalloc(rel)");
+  if (!ix.sparse)
+    TRYC(hipMalloc(&ix.rel, sizeof(uint32_t) * std::max<int64_t>(rel_elems, 1)), "hipMalloc(rel)");
   TRYC(hipMalloc(&ix.ldoc, sizeof(uint16_t) * (nnz + kPostingPad)), "hipMalloc(ldoc)");
   TRYC(hipMalloc(&ix.val, sizeof(float) * (nnz + kPostingPad)), "hipMalloc(val)");
   TRYC(hipMemsetAsync(ix.ldoc + nnz, 0, sizeof(uint16_t) * kPostingPad, h->stream), "hipMemset");
   TRYC(hipMemsetAsync(ix.val + nnz, 0, sizeof(float) * kPostingPad, h->stream), "hipMemset");
   TRYC(hipMalloc(&d_indices, sizeof(int32_t) * std::max<int64_t>(nnz, 1)), "hipMalloc(indices)");
   TRYC(hipMalloc(&d_err, sizeof(int32_t)), "hipMalloc(err)");
-  h->device_bytes = (int64_t)(sizeof(int64_t) * (n_terms + 1) + sizeof(uint32_t) * rel_elems +
+  h->device_bytes = (int64_t)(sizeof(int64_t) * (n_terms + 1) +
+                              (ix.sparse ? 0 : sizeof(uint32_t) * rel_elems) +
                               (sizeof(uint16_t) + sizeof(float)) * nnz);
   TRYC(hipMemsetAsync(d_err, 0, sizeof(int32_t), h->stream), "hipMemset");
   TRYC(hipMemcpyAsync(ix.indptr, ip.data(), sizeof(int64_t) * (n_terms + 1), hipMemcpyHostToDevice, h->stream), "H2D indptr");
@@ -343,7 +357,30 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     TRYC(hipMemcpyAsync(d_indices, indices, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, h->stream), "H2D indices");
     TRYC(hipMemcpyAsync(ix.val, data, sizeof(float) * nnz, hipMemcpyHostToDevice, h->stream), "H2D data");
   }
-  TRYC(launch_build_tables(ix, d_indices, d_err, h->stream), "build_tables launch");
+  if (!ix.sparse) {
+    TRYC(launch_build_tables(ix, d_indices, d_err, h->stream), "build_tables launch");
+  } else {  // tile lists: count per term, scan on the host, fill
+    int64_t* d_cnt = nullptr;
+    TRYC(hipMalloc(&d_cnt, sizeof(int64_t) * std::max<int64_t>(n_terms, 1)), "hipMalloc(cnt)");
+    std::vector<int64_t> cnt(n_terms + 1, 0);
+    e = launch_count_tiles(ix, d_indices, d_cnt, d_err, h->stream);
+    if (e == hipSuccess && n_terms > 0)
+      e = hipMemcpyAsync(cnt.data() + 1, d_cnt, sizeof(int64_t) * n_terms, hipMemcpyDeviceToHost,
+                         h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    hipFree(d_cnt);
+    if (e != hipSuccess) return cleanup(hip_fail(e, "count_tiles"));
+    for (int64_t t = 0; t < n_terms; ++t) cnt[t + 1] += cnt[t];
+    ix.n_pairs = cnt[n_terms];
+    TRYC(hipMalloc(&ix.tl_ptr, sizeof(int64_t) * (n_terms + 1)), "hipMalloc(tl_ptr)");
+    TRYC(hipMalloc(&ix.tl_tile, sizeof(uint16_t) * std::max<int64_t>(ix.n_pairs, 1)), "hipMalloc(tl_tile)");
+    TRYC(hipMalloc(&ix.tl_start, sizeof(uint32_t) * std::max<int64_t>(ix.n_pairs, 1)), "hipMalloc(tl_start)");
+    TRYC(hipMemcpyAsync(ix.tl_ptr, cnt.data(), sizeof(int64_t) * (n_terms + 1), hipMemcpyHostToDevice, h->stream), "H2D tl_ptr");
+    TRYC(launch_fill_tiles(ix, d_indices, h->stream), "fill_tiles launch");
+    TRYC(hipStreamSynchronize(h->stream), "fill_tiles");
+    h->device_bytes += (int64_t)(sizeof(int64_t) * (n_terms + 1) +
+                                 (sizeof(uint16_t) + sizeof(uint32_t)) * ix.n_pairs);
+  }
   // values 0 or normal positive (no NaN, no denormal): every doc's running
   // sum only grows and is 0 or >= FLT_MIN, which lets the REST pass flag
   // candidates while adding and complete rare queries with zero-score docs
@@ -379,6 +416,9 @@ int bm25_index_destroy(bm25_index* h) {
   hipFree(h->d_scores);
   hipFree(h->ix.indptr);
   hipFree(h->ix.rel);
+  hipFree(h->ix.tl_ptr);
+  hipFree(h->ix.tl_tile);
+  hipFree(h->ix.tl_start);
   hipFree(h->ix.ldoc);
   hipFree(h->ix.val);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -395,6 +435,13 @@ int bm25_index_info(const bm25_index* h, int64_t* n_docs, int64_t* n_terms, int6
   if (tile_docs) *tile_docs = 1 << h->ix.tile_shift;
   if (n_tiles) *n_tiles = h->ix.ntiles;
   if (device_bytes) *device_bytes = h->device_bytes;
+  return BM25_OK;
+}
+
+int bm25_index_segments(const bm25_index* h, int32_t* sparse, int64_t* n_pairs) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (sparse) *sparse = h->ix.sparse ? 1 : 0;
+  if (n_pairs) *n_pairs = h->ix.n_pairs;
   return BM25_OK;
 }
 

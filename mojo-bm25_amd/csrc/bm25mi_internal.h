@@ -65,7 +65,18 @@ struct DevIndex {
   bool nonneg = false;  // every CSC value is 0 or >= FLT_MIN (running sums are monotone)
   int64_t ntiles = 0;
   int64_t* indptr = nullptr;
+  // Segment table, dense or sparse: the postings of term t in
+  // tile j are [indptr[t] + r(t, j), indptr[t] + r(t, j + 1)) where
+  //   dense:  r(t, j) = rel[t * (ntiles + 1) + j]          (V x (ntiles+1) u32)
+  //   sparse: the term's non-empty tiles tl_tile[tl_ptr[t] .. tl_ptr[t+1])
+  //           (ascending u16) with their first postings tl_start (u32,
+  //           relative to indptr[t]) — O(non-empty (term, tile) pairs).
+  bool sparse = false;
   uint32_t* rel = nullptr;
+  int64_t* tl_ptr = nullptr;
+  uint16_t* tl_tile = nullptr;
+  uint32_t* tl_start = nullptr;
+  int64_t n_pairs = 0;
   uint16_t* ldoc = nullptr;
   float* val = nullptr;
 };
@@ -85,6 +96,9 @@ struct Workspace {
   int32_t* counters = nullptr;   // [0]/[1] rescore queue length / pop cursor,
                                  // [2] fallback queries, [3] tiles re-scored this search
   int32_t* wctr = nullptr;       // [kWctrInts] item-claim counters, zeroed before each score launch
+  uint64_t* seg = nullptr;       // sparse index: [Q][bands][64] segment of (tile, term) lanes of
+                                 // each band item (start | len << 32), built per search
+  int64_t cap_seg = 0;           // u64 entries of seg
 };
 
 // Flag slots per query: a flagged tile holds kTileM keys of the top-(k-1), so
@@ -107,6 +121,14 @@ SampleGeom sample_geom(int64_t ntiles, int k, int W);
 // Kernel launchers (bm25mi_kernels.hip).  All enqueue on `stream`.
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,
                                int32_t* d_err, hipStream_t stream);
+// Sparse segment table: non-empty tiles per term -> d_cnt[V] (also writes
+// ldoc and validates, as launch_build_tables), then (after the caller's scan
+// into ix.tl_ptr) the tile lists.
+hipError_t launch_count_tiles(const DevIndex& ix, const int32_t* d_indices, int64_t* d_cnt,
+                              int32_t* d_err, hipStream_t stream);
+hipError_t launch_fill_tiles(const DevIndex& ix, const int32_t* d_indices, hipStream_t stream);
+// u64 entries of Workspace::seg a search of Q queries needs (0: dense index).
+int64_t seg_entries(const DevIndex& ix, int64_t Q);
 // Score pass of a single-index search: SAMPLE + theta + REST (or the exact
 // pass when the index is too small to sample).
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,

@@ -52,11 +52,41 @@ struct IndexArgs {
   int64_t V, ntiles, n_docs, nnz;
   int64_t doc_offset;  // global id of the index's first doc (sample keys are global)
   int32_t nonneg;
+  int32_t sparse;           // segment table form (DevIndex)
+  const int64_t* tl_ptr;    // sparse: tile lists
+  const uint16_t* tl_tile;
+  const uint32_t* tl_start;
+  const uint64_t* seg;      // sparse + band kernel: this search's per-item segments
 };
 
 static IndexArgs args_of(const DevIndex& ix) {
   return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs,
-                   ix.nnz, ix.doc_offset, ix.nonneg ? 1 : 0};
+                   ix.nnz, ix.doc_offset, ix.nonneg ? 1 : 0, ix.sparse ? 1 : 0, ix.tl_ptr,
+                   ix.tl_tile, ix.tl_start, nullptr};
+}
+
+// Segment bounds [r0, r1) (relative to indptr[term]) of a valid term in a
+// tile.  Sparse: a binary search of the term's tile list (the cold paths; the
+// band kernel reads a per-search table instead, seg_table_kernel).
+__device__ __forceinline__ void segment(const IndexArgs& a, int64_t term, int64_t tile,
+                                        uint32_t& r0, uint32_t& r1) {
+  if (!a.sparse) {
+    const uint32_t* r = a.rel + term * (a.ntiles + 1) + tile;
+    r0 = r[0];
+    r1 = r[1];
+    return;
+  }
+  const int64_t b = a.tl_ptr[term], e = a.tl_ptr[term + 1];
+  int64_t lo = b, hi = e;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)a.tl_tile[mid] < tile) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint32_t df = (uint32_t)(a.indptr[term + 1] - a.indptr[term]);
+  const uint32_t at = lo < e ? a.tl_start[lo] : df;
+  r0 = r1 = at;
+  if (lo < e && (int64_t)a.tl_tile[lo] == tile) r1 = lo + 1 < e ? a.tl_start[lo + 1] : df;
 }
 
 // Sample tiles: groups of G consecutive tiles, one group in every G*P tiles
@@ -220,8 +250,8 @@ __device__ __forceinline__ void add_item(const IndexArgs& a, int64_t tile,
     if (lane < ng) {
       const int32_t term = qterms[g0 + lane];
       if (term >= 0 && term < a.V) {  // negative ids are padding (bm25_native.py:151)
-        const uint32_t* r = a.rel + (int64_t)term * (a.ntiles + 1) + tile;
-        const uint32_t r0 = r[0], r1 = r[1];
+        uint32_t r0, r1;
+        segment(a, term, tile, r0, r1);
         beg = a.indptr[term] + r0;
         len = r1 - r0;
       }
@@ -506,10 +536,8 @@ __device__ __forceinline__ Desc load_desc(const IndexArgs& a, int32_t term, int6
   Desc d;
   d.ok = term >= 0 && term < a.V;  // negative ids are padding (bm25_native.py:151)
   const int64_t t = d.ok ? term : 0;
-  const uint32_t* r = a.rel + t * (a.ntiles + 1) + tile;
   d.ip = a.indptr[t];
-  d.r0 = r[0];
-  d.r1 = r[1];
+  segment(a, t, tile, d.r0, d.r1);
   return d;
 }
 
@@ -1253,8 +1281,16 @@ __device__ __forceinline__ void issue_rows2(const PostingRsrc& pr, const Rows2& 
   }
 }
 
-template <int S, int PH, int SM>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 4))) void score_band_kernel(
+#ifndef BM25_BAND_WAVES
+#define BM25_BAND_WAVES 4
+#endif
+#ifndef BM25_BAND_WPE
+#define BM25_BAND_WPE 4
+#endif
+constexpr int kBandWaves = BM25_BAND_WAVES;  // independent waves per band workgroup
+
+template <int S, int PH, int SM, bool SP>
+__global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu(BM25_BAND_WPE, BM25_BAND_WPE))) void score_band_kernel(
     IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t G, int32_t nq,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int64_t cstride,
     uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
@@ -1262,7 +1298,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     const uint64_t* __restrict__ skeys, int64_t sstride) {
   constexpr int D = 1 << S;
   constexpr int DP = D + 64;
-  __shared__ __attribute__((aligned(16))) float acc_all[kWaves * DP];
+  __shared__ __attribute__((aligned(16))) float acc_all[kBandWaves * DP];
   const int wave = uniform((int)(threadIdx.x >> 6));
   float* acc = acc_all + wave * DP;
   const uint32_t lane = lane_id();
@@ -1275,10 +1311,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
   const uint32_t lo = (uint32_t)(grp * per);
   const int32_t ngi = (int32_t)max<int64_t>(0, min<int64_t>(nitems, lo + per) - lo);
   if (ngi == 0) return;  // wave-uniform; no barriers in this kernel
-  const int32_t cm = (int32_t)((blockIdx.x >> 3) * kWaves + wave) % claim_m;
+  const int32_t cm = (int32_t)((blockIdx.x >> 3) * kBandWaves + wave) % claim_m;
   int32_t* ctr = wctr + (grp * kClaimM + cm) * kCtrStride;
   const PostingRsrc pr = posting_rsrc(a);
   const uint32_t lt = lane & 7u, li = lane >> 3;  // segment lane: tile li, term lt
+  const int64_t nbp = (a.ntiles + 7) >> 3;          // physical bands (sparse seg rows)
 
   auto claim = [&]() -> int32_t {
     int32_t v = 0;
@@ -1326,10 +1363,18 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
     const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b * kBandW + li), (uint32_t)P,
                                                       (uint32_t)G)
                             : 0;
-    const uint32_t* r = a.rel + tt * (a.ntiles + 1) + tile;
-    d.ip = (uint32_t)a.indptr[tt];
-    d.r0 = r[0];
-    d.r1 = r[1];
+    if constexpr (SP) {  // this search's segment table (seg_table_kernel)
+      const uint64_t e =
+          ok ? a.seg[((int64_t)c.q * nbp + (tile >> 3)) * 64 + lt * 8 + (tile & 7)] : 0ull;
+      d.ip = 0u;
+      d.r0 = (uint32_t)e;
+      d.r1 = (uint32_t)e + (uint32_t)(e >> 32);
+    } else {
+      const uint32_t* r = a.rel + tt * (a.ntiles + 1) + tile;
+      d.ip = (uint32_t)a.indptr[tt];
+      d.r0 = r[0];
+      d.r1 = r[1];
+    }
     d.ok = ok ? 1u : 0u;
     const int64_t si = (int64_t)(c.b / P) * kBandW + min(li, (uint32_t)(c.bw - 1));
     d.skey = skipping ? skeys[(int64_t)c.q * sstride + min<int64_t>(si, sstride - 1)] : ~0ull;
@@ -1740,6 +1785,63 @@ __global__ __launch_bounds__(256) void build_tables_kernel(
   }
 }
 
+// Sparse segment table, pass 1: ldoc + validation (as build_tables_kernel)
+// and the number of non-empty tiles of every term (one wave per term).
+__global__ __launch_bounds__(256) void count_tiles_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t V,
+    int64_t n_docs, int S, uint16_t* __restrict__ ldoc, int64_t* __restrict__ cnt,
+    int32_t* __restrict__ err) {
+  const int lane = lane_id();
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const uint32_t mask = (1u << S) - 1u;
+  for (int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < V;
+       t += waves) {
+    const int64_t a0 = indptr[t], a1 = indptr[t + 1];
+    uint32_t n = 0;
+    for (int64_t p = a0 + lane; p < a1; p += 64) {
+      const int32_t d = indices[p];
+      const int32_t dp = p > a0 ? indices[p - 1] : -1;
+      const bool ok = d >= 0 && (int64_t)d < n_docs && d > dp;
+      if (!ok) atomicOr(err, 1);
+      ldoc[p] = (uint16_t)((uint32_t)d & mask);
+      n += (dp < 0 || (d >> S) != (dp >> S)) ? 1u : 0u;
+    }
+    const uint32_t tot = wave_incl_scan(n);
+    if (lane == 63) cnt[t] = (int64_t)tot;
+  }
+}
+
+// Pass 2: the tile lists (tl_ptr = exclusive scan of the counts).
+__global__ __launch_bounds__(256) void fill_tiles_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t V, int S,
+    const int64_t* __restrict__ tl_ptr, uint16_t* __restrict__ tl_tile,
+    uint32_t* __restrict__ tl_start) {
+  const int lane = lane_id();
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < V;
+       t += waves) {
+    const int64_t a0 = indptr[t], a1 = indptr[t + 1];
+    int64_t o = tl_ptr[t];
+    for (int64_t p0 = a0; p0 < a1; p0 += 64) {
+      const int64_t p = p0 + lane;
+      bool first = false;
+      int32_t d = 0;
+      if (p < a1) {
+        d = indices[p];
+        const int32_t dp = p > a0 ? indices[p - 1] : -1;
+        first = dp < 0 || (d >> S) != (dp >> S);
+      }
+      const uint64_t m = __ballot(first);
+      if (first) {
+        const int64_t i = o + __popcll(m & ((1ull << lane) - 1ull));
+        tl_tile[i] = (uint16_t)(d >> S);
+        tl_start[i] = (uint32_t)(p - a0);
+      }
+      o += __popcll(m);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Merge: one workgroup per query, bitonic sort of u64 keys in LDS.
 // ---------------------------------------------------------------------------
@@ -2042,6 +2144,23 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
   return hipGetLastError();
 }
 
+hipError_t launch_count_tiles(const DevIndex& ix, const int32_t* d_indices, int64_t* d_cnt,
+                              int32_t* d_err, hipStream_t stream) {
+  if (ix.n_terms == 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((ix.n_terms + 3) / 4, 65536);
+  hipLaunchKernelGGL(count_tiles_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, ix.indptr,
+                     d_indices, ix.n_terms, ix.n_docs, ix.tile_shift, ix.ldoc, d_cnt, d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_tiles(const DevIndex& ix, const int32_t* d_indices, hipStream_t stream) {
+  if (ix.n_terms == 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((ix.n_terms + 3) / 4, 65536);
+  hipLaunchKernelGGL(fill_tiles_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, ix.indptr,
+                     d_indices, ix.n_terms, ix.tile_shift, ix.tl_ptr, ix.tl_tile, ix.tl_start);
+  return hipGetLastError();
+}
+
 // Sampling geometry: 1 tile in P is a sample tile reporting m keys (the best
 // of each of m doc slices); the first (P, m) in the order P = BM25_SAMPLE_P
 // (default 8), 4, 2 (powers of two), m = 1, 2, 4 whose sample — over the W
@@ -2066,7 +2185,7 @@ SampleGeom sample_geom(int64_t ntiles, int k, int W) {
 // Every resident workgroup slot of the current device (a multiple of 8, one
 // per XCD round), cached per (kernel, device).
 template <int S, int PH, class K>
-static int persistent_grid(K kernel) {
+static int persistent_grid(K kernel, int block = 64 * kWaves) {
   static std::mutex mu;
   static std::map<std::pair<const void*, int>, int> cache;
   int dev = 0;
@@ -2077,7 +2196,7 @@ static int persistent_grid(K kernel) {
   if (it != cache.end()) return it->second;
   int cus = 0, occ = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 64 * kWaves, 0);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, 0);
   const char* e = getenv("BM25_WG_PER_CU");
   if (e) occ = atoi(e);
   const int g = ((cus * (occ > 0 ? occ : 1) + 7) / 8) * 8;
@@ -2181,15 +2300,68 @@ static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const S
       return;
     }
   }
-  const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM>);
   hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrInts, st);
   // REST skips the sample tiles whose best key is below theta (m = 1 samples
   // in groups of one band: ws.cand holds this shard's sample keys)
   const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kBandW;
-  hipLaunchKernelGGL((score_band_kernel<S, PH, SM>), dim3((unsigned)grid), dim3(64 * kWaves), 0,
-                     st, args_of(ix), q, (int32_t)T, sg.P, sg.G, sg.nq_host, ws.theta,
+  IndexArgs a = args_of(ix);
+  a.seg = ws.seg;
+  if (ix.sparse) {
+    const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM, true>, 64 * kBandWaves);
+    hipLaunchKernelGGL((score_band_kernel<S, PH, SM, true>), dim3((unsigned)grid),
+                       dim3(64 * kBandWaves), 0, st, a, q, (int32_t)T, sg.P, sg.G, sg.nq_host,
+                       ws.theta, sg.cand_out, sg.cstride, ws.list, ws.list_cnt, ws.list_cap,
+                       ws.wctr, band_claim(), claim_m(), skip ? sg.sample_keys : nullptr,
+                       sg.sample_stride);
+    return;
+  }
+  const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM, false>, 64 * kBandWaves);
+  hipLaunchKernelGGL((score_band_kernel<S, PH, SM, false>), dim3((unsigned)grid),
+                     dim3(64 * kBandWaves), 0, st, a, q, (int32_t)T, sg.P, sg.G, sg.nq_host, ws.theta,
                      sg.cand_out, sg.cstride, ws.list, ws.list_cnt, ws.list_cap, ws.wctr,
                      band_claim(), claim_m(), skip ? sg.sample_keys : nullptr, sg.sample_stride);
+}
+
+// Sparse index, band kernel: the segment of every (band item lane = tile li,
+// query term lt) of the batch, from the query terms' tile lists — one wave
+// per (query, term position) walks its term's non-empty tiles (coalesced
+// reads) and writes (start | len << 32) into seg[q][tile / 8][pos][tile % 8]
+// (a term's entries of one band are one 64-B run); seg was zeroed (empty
+// segments).
+__global__ __launch_bounds__(256) void seg_table_kernel(IndexArgs a,
+                                                        const int32_t* __restrict__ queries,
+                                                        int64_t Q, int32_t T,
+                                                        uint64_t* __restrict__ seg) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= Q * T) return;  // wave-uniform; no barriers
+  const int64_t q = w / T;
+  const int pos = (int)(w - q * T);
+  const int32_t term = queries[q * T + pos];
+  if (term < 0 || term >= a.V) return;
+  const int64_t nbp = (a.ntiles + 7) >> 3;
+  const int64_t b = a.tl_ptr[term], e = a.tl_ptr[term + 1];
+  const int64_t ip = a.indptr[term];
+  const uint32_t df = (uint32_t)(a.indptr[term + 1] - ip);
+  uint64_t* row = seg + q * nbp * 64;
+  for (int64_t i = b + lane_id(); i < e; i += 64) {
+    const uint32_t tile = a.tl_tile[i];
+    const uint32_t st = a.tl_start[i];
+    const uint32_t nx = i + 1 < e ? a.tl_start[i + 1] : df;
+    row[(int64_t)(tile >> 3) * 64 + pos * 8 + (tile & 7)] =
+        (uint64_t)(uint32_t)(ip + st) | ((uint64_t)(nx - st) << 32);
+  }
+}
+
+int64_t seg_entries(const DevIndex& ix, int64_t Q) {
+  return ix.sparse ? Q * ((ix.ntiles + 7) >> 3) * 64 : 0;
+}
+
+static void launch_seg_table(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
+                             const Workspace& ws, hipStream_t st) {
+  hipMemsetAsync(ws.seg, 0, sizeof(uint64_t) * seg_entries(ix, Q), st);
+  const int64_t waves = Q * T;
+  hipLaunchKernelGGL(seg_table_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
+                     args_of(ix), q, Q, (int32_t)T, ws.seg);
 }
 
 template <int S, int PH>
@@ -2267,6 +2439,7 @@ template <int S_>
 static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
                      const SampleGeom& g, uint64_t* keys, const Workspace& ws, hipStream_t st) {
   hipMemsetAsync(keys, 0, sizeof(uint64_t) * Q * g.S, st);
+  if (ix.sparse && use_band(ix, T)) launch_seg_table(ix, q, Q, T, ws, st);  // SAMPLE + REST
   Stage sg = main_stage(ix, Q, g.P, ws);
   sg.M = g.m;
   sg.G = g.G;

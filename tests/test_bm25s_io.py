@@ -73,3 +73,37 @@ def test_load_reference_fixture_directory():
     for name in ("indptr", "indices", "data"):
         assert np.array_equal(getattr(ix, name), g[name])
     assert ix.document(0)["text"] == "a cat is a feline and likes to purr"
+
+
+def test_shard_csc_int64_indptr_concatenates_to_full(tmp_path):
+    """bm25mi.shard: a bm25s directory with an int64 indptr (the config-5
+    form) cut into rank shards — every shard is canonical CSC with local ids,
+    and the shards together are the whole index (small column blocks force
+    the streaming path across block edges)."""
+    from bm25mi import shard
+    from bm25mi.bm25s_io import load_bm25s, save_bm25s
+    rng = np.random.default_rng(5)
+    N, V = 50_000, 300
+    cols = [np.sort(rng.choice(N, int(rng.integers(0, 3000)), replace=False)) for _ in range(V)]
+    ip = np.zeros(V + 1, np.int64)
+    ip[1:] = np.cumsum([len(c) for c in cols])
+    ix = np.concatenate(cols).astype(np.int32)
+    dt = rng.random(ix.size).astype(np.float32)
+    save_bm25s(str(tmp_path), ip, ix, dt, N, vocab={"a": 0})
+    assert load_bm25s(str(tmp_path)).indptr.dtype == np.int64
+    for W in (1, 3, 8):
+        parts = []
+        for r in range(W):
+            sip, six, sdt, n, lo, _ = shard.load_bm25s_shard(str(tmp_path), r, W)
+            assert sip.dtype == np.int64 and six.dtype == np.int32
+            a, b = shard.shard_bounds(N, W, r)
+            assert (lo, n) == (a, b - a)
+            if six.size:
+                assert six.min() >= 0 and six.max() < n
+            parts.append((sip, six, sdt, lo))
+            blk = shard.shard_csc(ip, ix, dt, a, b, block=777)
+            assert all(np.array_equal(x, y) for x, y in zip(blk, (sip, six, sdt)))
+        for t in range(V):
+            d = np.concatenate([p[1][p[0][t]:p[0][t + 1]] + p[3] for p in parts])
+            v = np.concatenate([p[2][p[0][t]:p[0][t + 1]] for p in parts])
+            assert np.array_equal(d, ix[ip[t]:ip[t + 1]]) and np.array_equal(v, dt[ip[t]:ip[t + 1]])

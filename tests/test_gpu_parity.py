@@ -284,6 +284,9 @@ def test_config3_full_batch_parity(gpu):
     {}, {"BM25_SAMPLE_P": "1"}, {"BM25_SAMPLE_P": "2"}, {"BM25_SAMPLE_P": "16"},
     {"BM25_LIST_CAP": "8"}, {"BM25_TILE_SHIFT": "10", "BM25_LIST_CAP": "40"},
     {"BM25_NO_PIPE": "1"}, {"BM25_NO_PIPE": "1", "BM25_LIST_CAP": "8"},
+    {"BM25_SEGMENTS": "sparse"}, {"BM25_SEGMENTS": "sparse", "BM25_SAMPLE_P": "1"},
+    {"BM25_SEGMENTS": "sparse", "BM25_NO_BAND": "1"},
+    {"BM25_SEGMENTS": "sparse", "BM25_LIST_CAP": "8", "BM25_TILE_SHIFT": "10"},
 ])
 def test_kernel_variants_bit_exact(gpu, variant, monkeypatch):
     """Every search configuration gives the oracle's bits: sampling strides
@@ -335,6 +338,10 @@ def test_bm25_dense_model_golden(gpu):
     corpus = [d.lower().split() for d in g["docs"].tolist()]
     m = bm25.BM25()
     m.fit(corpus)
+    # the GPU-built float64 matrix is the reference's, bit for bit
+    assert m.vocabulary == g["vocabulary"].tolist()
+    assert m.bm25_matrix.dtype == np.float64
+    assert np.array_equal(m.bm25_matrix, g["bm25_matrix"])
     for i, q in enumerate(g["queries"].tolist()):
         toks = q.lower().split()
         s = m.get_scores(toks)
@@ -532,3 +539,130 @@ def test_sharded_index_global_theta_ties_and_small_shards(gpu):
         sh = ShardedIndex(ip, ix, dt, N, devices=devs)
         _exact(sh.search(qq, k), oracle.search_c(N, ip, ix, dt, qq, k))
         sh.close()
+
+
+# ------------------------------------------------- GPU index build (§8(f) 2)
+def test_build_scores_lucene_animal_fixture(gpu):
+    """bm25_build_scores (lucene, device idf) rebuilds animal_index_bm25's CSC
+    from (doc, term, tf) triples: indptr, indices and every data bit."""
+    from bm25mi.scoring import build_scores
+    g = _load("animal.npz")
+    ip0, ix0 = g["indptr"].astype(np.int64), g["indices"]
+    terms = np.repeat(np.arange(len(ip0) - 1), np.diff(ip0)).astype(np.int32)
+    dl = np.bincount(ix0, minlength=int(g["n_docs"]))
+    perm = np.random.default_rng(3).permutation(len(ix0))  # any triple order
+    ip, ix, dt = build_scores(ix0[perm], terms[perm], np.ones(len(ix0), np.float32), dl,
+                              len(ip0) - 1, k1=1.5, b=0.75, method="lucene")
+    assert np.array_equal(ip, ip0) and np.array_equal(ix, ix0)
+    assert np.array_equal(dt.view(np.uint32), g["data"].view(np.uint32))
+
+
+@pytest.mark.parametrize("method", ["lucene", "bm25py"])
+def test_build_scores_random_corpus(gpu, method):
+    """A 20k-doc random corpus (Zipf token ids, repeated tokens): the GPU
+    build equals the numpy restatement bit for bit with the host idf, and
+    within 1 f32 ulp with the device idf; the built index then searches
+    bit-exactly against the oracle."""
+    from bm25mi.scoring import build_scores, triples_from_token_ids
+    rng = np.random.default_rng(11)
+    V = 3000
+    docs_tok = [np.minimum(rng.zipf(1.3, size=int(rng.integers(0, 300))) - 1, V - 1)
+                for _ in range(20_000)]
+    docs, terms, tfs, dl = triples_from_token_ids(docs_tok)
+    avgdl = float(np.mean(dl.tolist()))
+    df = np.bincount(terms, minlength=V)
+    idf = oracle.idf_numpy(df, len(dl))
+    ref = oracle.build_scores_numpy(docs, terms, tfs, dl, V, 1.2, 0.7, method, avgdl, idf=idf)
+    got = build_scores(docs, terms, tfs, dl, V, k1=1.2, b=0.7, method=method, idf=idf,
+                       want_f64=True)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+    assert np.array_equal(got[2].view(np.uint32), ref[2].view(np.uint32))
+    assert np.array_equal(got[3].view(np.uint64), ref[3].view(np.uint64))
+    dev = build_scores(docs, terms, tfs, dl, V, k1=1.2, b=0.7, method=method)
+    ulp = np.abs(dev[2].view(np.int32).astype(np.int64) - ref[2].view(np.int32))
+    assert ulp.max() <= 1 and np.mean(ulp == 0) > 0.999
+    q = rng.integers(-1, V, size=(40, 6)).astype(np.int32)
+    index = _idx(got[0], got[1], got[2], len(dl))
+    _exact(index.search(q, 50), oracle.search_c(len(dl), got[0], got[1], got[2], q, 50))
+
+
+def test_build_scores_rejects_bad_triples(gpu):
+    from bm25mi.scoring import build_scores
+    with pytest.raises(ValueError, match="duplicate"):
+        build_scores([0, 0], [1, 1], [1.0, 2.0], [3], 2)
+    with pytest.raises(ValueError, match="out of range"):
+        build_scores([0, 5], [1, 1], [1.0, 2.0], [3, 3], 2)
+    with pytest.raises(ValueError, match="positive"):
+        build_scores([0], [1], [0.0], [3], 2)
+    ip, ix, dt = build_scores([], [], [], [0, 0], 4)
+    assert np.array_equal(ip, np.zeros(5, np.int64)) and ix.size == 0
+
+
+# ------------------------------------------------- sparse segments / config 5
+def test_config3_sparse_segments_full_batch(gpu, monkeypatch):
+    """The headline batch on the O(pairs) segment table (tile lists + the
+    per-search seg table of the band kernel): all 1024 queries bit-exact."""
+    from bm25mi import synth
+    monkeypatch.setenv("BM25_SEGMENTS", "sparse")
+    cfg = synth.CONFIGS["c3"]
+    ip, ix, dt = synth.make_index(cfg, threads=16)
+    q = synth.make_queries(cfg)
+    index = _idx(ip, ix, dt, cfg.n_docs)
+    info = index.info()
+    assert info["sparse"] and 0 < info["n_pairs"] <= len(ix)
+    assert info["device_bytes"] < 6 * len(ix) + 2_000_000_000  # no dense V x ntiles table
+    _exact(index.search(q, cfg.k), oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k, threads=16))
+
+
+def test_config5_shape_int64_shards_sparse(gpu, tmp_path, monkeypatch):
+    """Config 5 in miniature: a collection written as a bm25s directory with
+    an int64 indptr, cut per rank by bm25mi.shard (streamed column blocks),
+    each rank's shard on the sparse segment table (chosen automatically:
+    its vocabulary is large for its tile count), searched with the global
+    threshold protocol and merged — bit-exact vs the oracle on the whole
+    collection."""
+    import torch
+    from bm25mi import synth
+    from bm25mi.bm25s_io import save_bm25s
+    from bm25mi.shard import load_bm25s_shard
+    from bm25mi.index import GpuIndex, merge_topk_device
+    from bm25mi.dist import sharded_search
+    cfg = synth.Config("c5-mini", 2_000_000, 400_000, 16_000_000, 128, 8, 100)
+    ip, ix, dt = synth.make_index(cfg, threads=16)
+    q = synth.make_queries(cfg)
+    save_bm25s(str(tmp_path), ip.astype(np.int64), ix, dt, cfg.n_docs)
+    W = 4
+    dq = torch.from_numpy(q).cuda()
+    st = torch.cuda.current_stream()
+    shards, sdm = [], 0
+    for r in range(W):
+        sip, six, sdt, n, lo, _ = load_bm25s_shard(str(tmp_path), r, W)
+        sh = GpuIndex(sip, six, sdt, n, doc_offset=lo)
+        assert sh.info()["sparse"]  # chosen automatically (V x ntiles > 2x postings)
+        shards.append(sh)
+        sdm = max(sdm, n)
+    ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k, threads=16)
+    keys = []
+    for sh in shards:
+        S = sh.sample_width(cfg.k, W, sdm)
+        kk = torch.zeros((len(q), max(S, 1)), dtype=torch.int64, device="cuda")
+        if S > 0:
+            sh.search_sample_device(dq, cfg.k, W, sdm, kk, st)
+        keys.append(kk)
+    all_keys = torch.stack(keys)
+
+    class Ex:
+        world = W
+
+        def __call__(self, _):
+            return all_keys
+
+    lists_d = torch.empty((W, len(q), cfg.k), dtype=torch.int32, device="cuda")
+    lists_s = torch.empty((W, len(q), cfg.k), dtype=torch.float32, device="cuda")
+    for r, sh in enumerate(shards):
+        sharded_search(sh, dq, cfg.k, sdm, lists_d[r], lists_s[r], None, st, exchange=Ex())
+    md = torch.empty((len(q), cfg.k), dtype=torch.int32, device="cuda")
+    ms = torch.empty((len(q), cfg.k), dtype=torch.float32, device="cuda")
+    merge_topk_device(0, lists_d, lists_s, W, len(q), cfg.k, md, ms, st)
+    torch.cuda.synchronize()
+    _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)

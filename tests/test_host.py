@@ -145,10 +145,10 @@ def test_sharded_create_without_gpu_fails_loudly():
                      np.array([1.0], np.float32), 1, devices=[0, 0])
 
 
-def test_bm25_fit_matrix_matches_reference():
-    """bm25.BM25.fit (drop-in) builds the reference's float64 matrix bit for
-    bit (golden bm25_dense.npz from bm25.py); the GPU upload that follows
-    fails loudly without a GPU."""
+def test_bm25_fit_builds_on_the_gpu_only():
+    """bm25.BM25.fit builds its matrix with bm25_build_scores: without a GPU
+    it fails loudly (no host fallback); the matrix itself is checked against
+    the reference in tests/test_gpu_parity.py."""
     import os
     import bm25
     from bm25mi._capi import HipError
@@ -156,14 +156,19 @@ def test_bm25_fit_matrix_matches_reference():
     g = np.load(os.path.join(GOLDEN, "bm25_dense.npz"), allow_pickle=False)
     corpus = [d.lower().split() for d in g["docs"].tolist()]
     m = bm25.BM25()
-    try:
-        m.fit(corpus)
-    except HipError:
-        assert not gpu_available()
+    if not gpu_available():
+        with pytest.raises(HipError, match="no HIP device"):
+            m.fit(corpus)
     assert m.vocabulary == g["vocabulary"].tolist()
-    assert m.bm25_matrix.dtype == np.float64
-    assert np.array_equal(m.bm25_matrix, g["bm25_matrix"])
     assert bm25.BM25().get_top_n(["x"], corpus, n=0) == []
     e = bm25.BM25()
     e.fit([])
     assert e.get_scores(["a"]).shape == (0,)
+
+
+def test_build_scores_validation_without_gpu():
+    from bm25mi.scoring import build_scores
+    with pytest.raises(ValueError, match="method"):
+        build_scores([0], [0], [1.0], [1], 1, method="okapi")
+    with pytest.raises(ValueError, match="same length"):
+        build_scores([0, 1], [0], [1.0], [1, 1], 1)

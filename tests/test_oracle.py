@@ -147,3 +147,42 @@ def test_faithful_k_too_large_raises():
     with pytest.raises(ValueError, match="out of bounds"):
         oracle.search_faithful(4, g["indptr"], g["indices"], g["data"],
                                np.array([[0]], np.int32), 5)
+
+
+def _animal_triples():
+    """(doc, term, tf=1) triples and document lengths of animal_index_bm25
+    (every term occurs once per document there: dl = postings per doc)."""
+    g = np.load(os.path.join(GOLDEN, "animal.npz"), allow_pickle=False)
+    ip, ix = g["indptr"].astype(np.int64), g["indices"]
+    terms = np.repeat(np.arange(len(ip) - 1), np.diff(ip))
+    dl = np.bincount(ix, minlength=int(g["n_docs"]))
+    return g, ix, terms, np.ones(len(ix), np.float32), dl
+
+
+def test_build_scores_lucene_restatement_matches_fixture():
+    """The lucene build rule (bm25s writer) reproduces every value of
+    animal_index_bm25/data.csc.index.npy bit for bit."""
+    g, docs, terms, tfs, dl = _animal_triples()
+    ip, ix, d32, _ = oracle.build_scores_numpy(docs, terms, tfs, dl, len(g["indptr"]) - 1,
+                                               1.5, 0.75, "lucene", float(np.mean(dl)))
+    assert np.array_equal(ip, g["indptr"]) and np.array_equal(ix, g["indices"])
+    assert np.array_equal(d32.view(np.uint32), g["data"].view(np.uint32))
+
+
+def test_build_scores_bm25py_restatement_matches_reference_matrix():
+    """The bm25.py build rule reproduces the reference's float64 bm25_matrix
+    (golden bm25_dense.npz, generated by importing bm25.py) bit for bit."""
+    from collections import Counter
+    import scipy.sparse as sp
+    g = np.load(os.path.join(GOLDEN, "bm25_dense.npz"), allow_pickle=False)
+    corpus = [d.lower().split() for d in g["docs"].tolist()]
+    tid = {t: i for i, t in enumerate(g["vocabulary"].tolist())}
+    docs, terms, tfs = [], [], []
+    for i, d in enumerate(corpus):
+        for t, c in Counter(d).items():
+            docs.append(i), terms.append(tid[t]), tfs.append(c)
+    dl = [len(d) for d in corpus]
+    ip, ix, _, d64 = oracle.build_scores_numpy(docs, terms, tfs, dl, len(tid), 1.5, 0.75,
+                                               "bm25py", np.mean(dl))
+    m = sp.csc_matrix((d64, ix, ip), shape=(len(corpus), len(tid))).toarray()
+    assert np.array_equal(m, g["bm25_matrix"])
