@@ -1198,8 +1198,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
 // ===========================================================================
 constexpr int kBandT = 8;    // terms served (T <= kBandT)
 constexpr int kBandW = 8;    // tiles per band item
+#ifndef BM25_BAND_ABL  // dev ablations of the band kernel (timing only, wrong results)
+#define BM25_BAND_ABL 0
+#endif
 #ifndef BM25_KJ2
-#define BM25_KJ2 3
+#define BM25_KJ2 2
 #endif
 constexpr int kJ2 = BM25_KJ2;  // double rows per streamed block
 #ifndef BM25_NB
@@ -1269,8 +1272,19 @@ __device__ __forceinline__ Rows2 make_rows2(uint32_t beg, uint32_t len, int T, u
 // the config-3 score pass slower: 5.12 vs 4.75 ms.)
 __device__ __forceinline__ void issue_rows2(const PostingRsrc& pr, const Rows2& R, int j0,
                                             uint32_t (&ld)[kJ2], float (&v0)[kJ2],
-                                            float (&v1)[kJ2]) {
+                                            float (&v1)[kJ2], bool abl = false) {
   const uint32_t lane = lane_id();
+#if BM25_BAND_ABL & 1  // dev ablation: no posting loads (slots = the lane's own pair)
+  if (abl) {
+#pragma unroll
+    for (int j = 0; j < kJ2; ++j) {
+      ld[j] = (2u * lane + (uint32_t)j * 128u) | ((2u * lane + 1u + (uint32_t)j * 128u) << 16);
+      v0[j] = 1.f;
+      v1[j] = 1.f;
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < kJ2; ++j) {
     const uint32_t base = lane_u32(R.base, j0 + j);
@@ -1282,10 +1296,10 @@ __device__ __forceinline__ void issue_rows2(const PostingRsrc& pr, const Rows2& 
 }
 
 #ifndef BM25_BAND_WAVES
-#define BM25_BAND_WAVES 4
+#define BM25_BAND_WAVES 1
 #endif
 #ifndef BM25_BAND_WPE
-#define BM25_BAND_WPE 4
+#define BM25_BAND_WPE 5
 #endif
 constexpr int kBandWaves = BM25_BAND_WAVES;  // independent waves per band workgroup
 
@@ -1421,7 +1435,7 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
   uint32_t ltD[kNB][kJ2];
   float vD0[kNB][kJ2], vD1[kNB][kJ2];
 #pragma unroll
-  for (int k = 0; k < kNB; ++k) issue_rows2(pr, rD, k * kJ2, ltD[k], vD0[k], vD1[k]);
+  for (int k = 0; k < kNB; ++k) issue_rows2(pr, rD, k * kJ2, ltD[k], vD0[k], vD1[k], PH == kRest);
   BandCur nx3 = nx2;
   int32_t tmN3 = tmN2;
 
@@ -1449,7 +1463,7 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
       uint32_t ltC[kNB][kJ2];
       float vC0[kNB][kJ2], vC1[kNB][kJ2];
 #pragma unroll
-      for (int k = 0; k < kNB; ++k) issue_rows2(pr, rC, k * kJ2, ltC[k], vC0[k], vC1[k]);
+      for (int k = 0; k < kNB; ++k) issue_rows2(pr, rC, k * kJ2, ltC[k], vC0[k], vC1[k], PH == kRest);
 
       const uint64_t th = tab.th;
       const float thf_raw = key_score((uint32_t)(th >> 32));
@@ -1475,6 +1489,15 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
           v1[j] = m1 ? v1[j] : 0.f;
         }
         if (n == 0) return;
+#if BM25_BAND_ABL & 2  // dev ablation: no LDS adds (loads consumed by the hit flags)
+        if (PH == kRest) {
+#pragma unroll
+        for (int j = 0; j < kJ2; ++j)
+          if ((uint32_t)j < n)
+            hit |= __ballot(v0[j] + v1[j] + (float)ld[j] >= 1e30f);
+        return;
+        }
+#endif
         float x0 = acc[ld[0] & 0xFFFFu], x1 = acc[ld[0] >> 16];
 #pragma unroll
         for (int j = 0; j < kJ2; ++j) {
@@ -1503,6 +1526,9 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
         block(rD, k * kJ2, ltD[k], vD0[k], vD1[k],
               nrD > (uint32_t)(k * kJ2) ? min(nrD - k * kJ2, (uint32_t)kJ2) : 0u);
 
+#if BM25_BAND_ABL & 4  // dev ablation: REST emits nothing
+      if (PH == kRest) hit = 0;
+#endif
       if (nrD > kNB * kJ2) {
         // ---- a heavy tile: the remaining rows, block j + kJ2 always issued
         // before block j's adds (past the end: posting 0); dense selection
@@ -1510,7 +1536,7 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
         if (((kNB * kJ2) & 63) == 0) t = tile_rows(tab, i, kNB * kJ2);
         uint32_t ltY[kJ2];
         float vY0[kJ2], vY1[kJ2];
-        issue_rows2(pr, t, (kNB * kJ2) & 63, ltY, vY0, vY1);
+        issue_rows2(pr, t, (kNB * kJ2) & 63, ltY, vY0, vY1, PH == kRest);
         for (uint32_t j = kNB * kJ2; j < nrD; j += kJ2) {
           const uint32_t jn = j + kJ2;
           Rows2 tn = t;
@@ -1521,7 +1547,7 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
           }
           uint32_t ltZ[kJ2];
           float vZ0[kJ2], vZ1[kJ2];
-          issue_rows2(pr, tn, (int)(jn & 63), ltZ, vZ0, vZ1);
+          issue_rows2(pr, tn, (int)(jn & 63), ltZ, vZ0, vZ1, PH == kRest);
           block(t, (int)(j & 63), ltY, vY0, vY1, min(nrD - j, (uint32_t)kJ2));
           t = tn;
 #pragma unroll

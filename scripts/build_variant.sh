@@ -7,5 +7,5 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 mkdir -p exp
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result -Wno-unused-value "$@" \
-  -o exp/libbm25mi_$name.so mojo-bm25_amd/csrc/bm25mi_kernels.hip mojo-bm25_amd/csrc/bm25mi_capi.cpp
+  -o exp/libbm25mi_$name.so mojo-bm25_amd/csrc/bm25mi_kernels.hip mojo-bm25_amd/csrc/bm25mi_build.hip mojo-bm25_amd/csrc/bm25mi_capi.cpp
 echo exp/libbm25mi_$name.so
