@@ -55,7 +55,10 @@ constexpr int kCtrStride = 64;
 // Item order of the pipelined score kernel: bands of kBand consecutive tiles,
 // query by query inside a band; sample tiles in groups of kSampleGroup.
 constexpr int kBand = 8;
-constexpr int kSampleGroup = 8;
+#ifndef BM25_BANDW  // tiles per band item of the band kernel (4 or 8)
+#define BM25_BANDW 8
+#endif
+constexpr int kSampleGroup = BM25_BANDW;
 constexpr int kWctrInts = 8 * kClaimM * kCtrStride;
 
 struct DevIndex {

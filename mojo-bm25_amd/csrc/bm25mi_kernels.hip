@@ -1197,9 +1197,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 
 // csc_matvec).
 // ===========================================================================
 constexpr int kBandT = 8;    // terms served (T <= kBandT)
-constexpr int kBandW = 8;    // tiles per band item
+constexpr int kBandW = BM25_BANDW;  // tiles per band item
 #ifndef BM25_BAND_ABL  // dev ablations of the band kernel (timing only, wrong results)
 #define BM25_BAND_ABL 0
+#endif
+#ifndef BM25_HL  // row blocks in flight ahead of the adds in a heavy tile (1 or 2)
+#define BM25_HL 1
 #endif
 #ifndef BM25_KJ2
 #define BM25_KJ2 2
@@ -1537,9 +1540,28 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
         uint32_t ltY[kJ2];
         float vY0[kJ2], vY1[kJ2];
         issue_rows2(pr, t, (kNB * kJ2) & 63, ltY, vY0, vY1, PH == kRest);
+#if BM25_HL == 2
+        // a second block in flight: rows kNB * kJ2 + kJ2 .. (dead past the end)
+        Rows2 tw = t;
+        {
+          const uint32_t jw = kNB * kJ2 + kJ2;
+          if (jw < nrD && (jw & 63) == 0) tw = tile_rows(tab, i, jw);
+          if (jw >= nrD) {
+            tw.base = kNoRow;
+            tw.hi = 0u;
+          }
+        }
+        uint32_t ltW[kJ2];
+        float vW0[kJ2], vW1[kJ2];
+        issue_rows2(pr, tw, (int)((kNB * kJ2 + kJ2) & 63), ltW, vW0, vW1, PH == kRest);
+#endif
         for (uint32_t j = kNB * kJ2; j < nrD; j += kJ2) {
-          const uint32_t jn = j + kJ2;
+          const uint32_t jn = j + BM25_HL * kJ2;
+#if BM25_HL == 2
+          Rows2 tn = tw;
+#else
           Rows2 tn = t;
+#endif
           if (jn < nrD && (jn & 63) == 0) tn = tile_rows(tab, i, jn);
           if (jn >= nrD) {  // nothing left: a dead block keeps the load count static
             tn.base = kNoRow;
@@ -1549,6 +1571,19 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
           float vZ0[kJ2], vZ1[kJ2];
           issue_rows2(pr, tn, (int)(jn & 63), ltZ, vZ0, vZ1, PH == kRest);
           block(t, (int)(j & 63), ltY, vY0, vY1, min(nrD - j, (uint32_t)kJ2));
+#if BM25_HL == 2
+          t = tw;
+          tw = tn;
+#pragma unroll
+          for (int u = 0; u < kJ2; ++u) {
+            ltY[u] = ltW[u];
+            vY0[u] = vW0[u];
+            vY1[u] = vW1[u];
+            ltW[u] = ltZ[u];
+            vW0[u] = vZ0[u];
+            vW1[u] = vZ1[u];
+          }
+#else
           t = tn;
 #pragma unroll
           for (int u = 0; u < kJ2; ++u) {
@@ -1556,6 +1591,7 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
             vY0[u] = vZ0[u];
             vY1[u] = vZ1[u];
           }
+#endif
         }
         if (flagged && hit == 0)
           zero_acc<S>(acc);
@@ -2157,7 +2193,16 @@ __global__ __launch_bounds__(kMergeNT) void merge_lists_kernel(
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
+#ifdef BM25_S12
+#define BM25_CASE12(call) case 12: call(12); break;
+#else
+#define BM25_CASE12(call)
+#endif
+#ifdef BM25_S12  // dev: 4096-doc tiles (timing experiments)
+bool tile_shift_supported(int s) { return s == 10 || s == 11 || s == 12; }
+#else
 bool tile_shift_supported(int s) { return s == 10 || s == 11; }
+#endif
 
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int32_t* d_err,
                                hipStream_t stream) {
@@ -2507,6 +2552,7 @@ static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   switch (ix.tile_shift) {                               \
     case 10: call(10); break;                            \
     case 11: call(11); break;                            \
+    BM25_CASE12(call)                                    \
     default: return hipErrorInvalidValue;                \
   }
 
@@ -2590,6 +2636,9 @@ hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query, int64
   const dim3 grid((unsigned)ix.ntiles);
   switch (ix.tile_shift) {
     case 10: hipLaunchKernelGGL(scores_dense_kernel<10>, grid, dim3(64), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
+#ifdef BM25_S12
+    case 12: hipLaunchKernelGGL(scores_dense_kernel<12>, grid, dim3(64), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
+#endif
     case 11: hipLaunchKernelGGL(scores_dense_kernel<11>, grid, dim3(64), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
     default: return hipErrorInvalidValue;
   }
