@@ -15,8 +15,10 @@ columns with numpy; scores agree to ~1e-7 relative (north_star tolerance
 1e-4) and are returned as float64 arrays like the reference's.  Documents with
 equal scores are ranked by index ascending (the reference's
 ``argsort(...)[::-1]`` order among ties is implementation-defined).
-``get_top_n`` serves n <= 4096 (kMaxK) and raises ValueError above it, where
-the reference returns every document in order.
+``get_top_n`` with n <= 4096 (kMaxK) runs the engine's batched top-k; above
+it (the reference, bm25.py:172-178, ranks every document) the GPU's dense
+per-document scores are ranked by (score desc, index asc) — the ordering of
+an output vector, as the reference's own argsort.
 """
 from __future__ import annotations
 
@@ -136,10 +138,11 @@ class BM25:
         num = min(n, self.corpus_size)
         ids = self._query_ids(query)
         if num > MAX_TOP_K:
-            # deviation: the reference (bm25.py:172-178) argsorts every score;
-            # the engine's top-k stops at kMaxK (use get_scores for a full ranking)
-            raise ValueError(f"get_top_n: n={num} exceeds the engine's top-k limit {MAX_TOP_K}; "
-                             "rank get_scores() instead")
+            # past the engine's top-k limit: rank the GPU's dense scores
+            # (bm25.py:172-178 argsorts every score)
+            scores = self.get_scores(query).astype(np.float32)
+            order = np.lexsort((np.arange(self.corpus_size), -scores))[:num]
+            return [(np.float64(scores[d]), corpus[int(d)]) for d in order]
         q = np.full((1, max(len(ids), 1)), -1, np.int32)
         q[0, :len(ids)] = ids
         docs, scores = self._gpu.search(q, num)

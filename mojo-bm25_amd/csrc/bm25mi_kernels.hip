@@ -835,7 +835,9 @@ __device__ __forceinline__ void best_sparse(float* acc, const uint32_t (&l0)[kJ]
 // Dense form (heavier items): every accumulator of the tile (docs past n_docs
 // excluded), then the accumulators are cleared.  Lane entries are in doc
 // order inside each lane (entry_doc), so a slice is a contiguous run of them.
-template <int S, int M>
+// POS: only positive sums are keyed (a tile without one reports key 0), as the
+// touched-slot form.
+template <int S, int M, bool POS = false>
 __device__ __forceinline__ void best_dense(float* acc, int64_t tile, int64_t n_docs,
                                            uint32_t idoff, uint64_t* __restrict__ out) {
   constexpr int E = (1 << S) / 64;  // entries per lane
@@ -859,7 +861,8 @@ __device__ __forceinline__ void best_dense(float* acc, int64_t tile, int64_t n_d
       const float fe[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const uint32_t key = entry_key(fe[c], 4 * j + c, lane, lim);
+        const uint32_t key =
+            (POS && !(fe[c] > 0.f)) ? 0u : entry_key(fe[c], 4 * j + c, lane, lim);
         if (key > bk[i]) {
           bk[i] = key;
           bd[i] = entry_doc(4 * j + c, lane);
@@ -1705,6 +1708,357 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
   }
 }
 
+// ===========================================================================
+// Flat score kernel (queries of 1..8 terms; SAMPLE and REST).  DESIGN.md §4.
+//
+// The band kernel's items — (query, band of up to 8 phase tiles), claimed per
+// XCD — but the wave streams the posting rows of all its items as ONE
+// sequence that ignores tile and item boundaries:
+//   * an item's rows (double rows, each inside one (tile, term) segment;
+//     tile-major, query-term order inside a tile) are numbered once per item
+//     by a scan over its 64 (tile, term) segments; a CHUNK of up to 64 rows is
+//     one table, lane r = row r (flat_chunk: a binary search of the scan);
+//   * a ring of kFR rows is in flight: the step that adds row r issues row
+//     r + kFR into the registers row r freed, so loads never pause at a tile
+//     or item edge and every step issues the same loads (static vmcnt);
+//   * a row of another tile than the accumulator's first runs that tile's
+//     epilogue (REST: the keys >= theta, or a plain clear when no add reached
+//     theta; SAMPLE: the tile's best key per slice).
+// Per tile there is no row-table work, no refill of the pipeline and no
+// per-tile branch structure: the per-item fixed cost of the band kernel
+// (ablation: 2.49 of its 4.35 ms with no loads, adds or emission) is what
+// this removes.  Each doc's adds stay in query-term order (bm25_native.py:152).
+// ===========================================================================
+constexpr int kFR = 4;                       // rows in flight (ring slots)
+constexpr uint32_t kDeadSid = 0xFFFFFFFFu;   // padding row: no adds, no tile
+constexpr uint32_t kNoTag = 0xFFFFFFFFu;     // accumulator holds no tile
+
+#ifndef BM25_FLAT_WPE
+#define BM25_FLAT_WPE 5
+#endif
+
+// Inclusive prefix sum over the wave (DPP: rows of 16, then the row carries).
+__device__ __forceinline__ uint32_t scan64(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); // row_bcast:31
+  return x;
+}
+
+struct FlatTab {    // one chunk of an item's rows: lane r = row j0 + r
+  uint32_t base;    // even posting index of the row's first pair (0: dead row)
+  uint32_t off;     // base - segment start: lane l holds segment postings off + 2l, off + 2l + 1
+  uint32_t len;     // segment length (0: every lane masked)
+  uint32_t sid;     // (item serial << 6) | tile * 8 + term; kDeadSid: padding
+};
+
+struct FlatCtx {    // the item a chunk (or the accumulator's tile) belongs to
+  int32_t q, b;
+  uint64_t th;
+};
+
+// Rows [j0, j0 + 64) of an item whose (tile, term) lane s holds segment
+// [sb, sb + sl), rows [excl, incl) of the item.
+__device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t incl,
+                                              uint32_t excl, uint32_t total, uint32_t j0,
+                                              uint32_t ser) {
+  const uint32_t lane = lane_id();
+  const uint32_t j = j0 + lane;
+  int pos = 0;  // segments ending at or before row j (binary lifting)
+#pragma unroll
+  for (int step = 32; step >= 1; step >>= 1) {
+    const uint32_t x = (uint32_t)__shfl((int)incl, pos + step - 1, 64);
+    if (x <= j) pos += step;
+  }
+  const uint32_t e = (uint32_t)__shfl((int)excl, pos, 64);
+  const uint32_t b = (uint32_t)__shfl((int)sb, pos, 64);
+  const uint32_t l = (uint32_t)__shfl((int)sl, pos, 64);
+  const bool in = j < total;
+  FlatTab t;
+  t.base = (in && l != 0u) ? (b & ~1u) + 128u * (j - e) : 0u;
+  t.off = t.base - b;
+  t.len = in ? l : 0u;
+  t.sid = in ? (ser << 6) | (uint32_t)pos : kDeadSid;
+  return t;
+}
+
+template <int S, int PH, int SM, bool SP>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WPE, BM25_FLAT_WPE))) void score_flat_kernel(
+    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t G, int32_t nq,
+    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int64_t cstride,
+    uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
+    int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
+    const uint64_t* __restrict__ skeys, int64_t sstride) {
+  constexpr int D = 1 << S;
+  __shared__ __attribute__((aligned(16))) float acc[D + 64];
+  const uint32_t lane = lane_id();
+  const uint32_t trash = (uint32_t)D + lane;  // this lane's always-zero slot
+  const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
+  const int32_t nb = (nt + kBandW - 1) / kBandW;
+  const int64_t nitems = (int64_t)nb * nq;
+  const int64_t per = (nitems + 7) >> 3;
+  const int grp = (int)(blockIdx.x & 7);
+  const uint32_t lo = (uint32_t)(grp * per);
+  const int32_t ngi = (int32_t)max<int64_t>(0, min<int64_t>(nitems, lo + per) - lo);
+  if (ngi == 0) return;  // wave-uniform; no barriers in this kernel
+  const int32_t cm = (int32_t)(blockIdx.x >> 3) % claim_m;
+  int32_t* ctr = wctr + (grp * kClaimM + cm) * kCtrStride;
+  const PostingRsrc pr = posting_rsrc(a);
+  const uint32_t lt = lane & 7u, li = lane >> 3;  // segment lane: tile li, term lt
+  const int64_t nbp = (a.ntiles + 7) >> 3;          // physical bands (sparse seg rows)
+
+  // ---- items: claims, terms -> segment descriptors (as score_band_kernel)
+  auto claim = [&]() -> int32_t {
+    int32_t v = 0;
+    if (lane == 0) v = atomicAdd(ctr, 1);
+    return v;
+  };
+  int32_t pending = claim();
+  auto next = [&](BandCur c) -> BandCur {
+    if (c.rit >= ngi) return c;
+    if (c.rit + 1 < c.end) {
+      ++c.rit;
+      if (++c.q == nq) {
+        c.q = 0;
+        ++c.b;
+        c.bw = min(kBandW, nt - c.b * kBandW);
+      }
+      return c;
+    }
+    const int64_t bb = ((int64_t)uniform(pending) * claim_m + cm) * claim_ch;
+    if (bb >= ngi) {
+      c.rit = c.end = ngi;
+      return c;
+    }
+    pending = claim();
+    BandCur n;
+    n.rit = (int32_t)bb;
+    n.end = (int32_t)min<int64_t>(ngi, bb + claim_ch);
+    const uint32_t it = lo + (uint32_t)bb;
+    n.b = (int32_t)(it / (uint32_t)nq);
+    n.q = (int32_t)(it - (uint32_t)n.b * (uint32_t)nq);
+    n.bw = min(kBandW, nt - n.b * kBandW);
+    return n;
+  };
+  auto terms_of = [&](const BandCur& c) -> int32_t {
+    return queries[(int64_t)c.q * T + (int)min(lt, (uint32_t)(T - 1))];
+  };
+  const bool skipping = PH == kRest && skeys != nullptr && G == kBandW;
+  auto load_bdesc = [&](const BandCur& c, int32_t tm) -> BandDesc {
+    BandDesc d;
+    const int32_t term = __shfl(tm, (int)lt, 64);
+    const bool ok = (int)lt < T && (int)li < c.bw && term >= 0 && term < a.V;
+    const int64_t tt = ok ? term : 0;
+    const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b * kBandW + li), (uint32_t)P,
+                                                      (uint32_t)G)
+                            : 0;
+    if constexpr (SP) {
+      const uint64_t e =
+          ok ? a.seg[((int64_t)c.q * nbp + (tile >> 3)) * 64 + lt * 8 + (tile & 7)] : 0ull;
+      d.ip = 0u;
+      d.r0 = (uint32_t)e;
+      d.r1 = (uint32_t)e + (uint32_t)(e >> 32);
+    } else {
+      const uint32_t* r = a.rel + tt * (a.ntiles + 1) + tile;
+      d.ip = (uint32_t)a.indptr[tt];
+      d.r0 = r[0];
+      d.r1 = r[1];
+    }
+    d.ok = ok ? 1u : 0u;
+    const int64_t si = (int64_t)(c.b / P) * kBandW + min(li, (uint32_t)(c.bw - 1));
+    d.skey = skipping ? skeys[(int64_t)c.q * sstride + min<int64_t>(si, sstride - 1)] : ~0ull;
+    if (!(skipping && (c.b % P) == 0)) d.skey = ~0ull;
+    return d;
+  };
+  auto th_positive = [&](uint64_t th) -> bool {
+    return (uint32_t)(th >> 32) > score_key(0.f);
+  };
+
+  // ---- the issue side's item: its segments (lane s = tile * 8 + term) and
+  // row numbering; the item prefetch pipeline one and two items ahead
+  uint32_t iSb = 0, iSl = 0, iIncl = 0, iExcl = 0;
+  uint32_t iTotal = 0, iR = 0, iJ0 = 0, iSer = 0;
+  FlatCtx ctxI{0, 0, 0ull};
+  BandCur nx, nx2;
+  BandDesc dN;
+  uint64_t thN = 0ull;
+  int32_t tmN2 = 0;
+  // enter item nx (descriptors dN) on the issue side; advance the prefetch
+  auto enter_item = [&]() {
+    const bool th_pos = PH == kRest && th_positive(thN);
+    const bool skip = skipping && th_pos && (uint32_t)(dN.skey >> 32) < (uint32_t)(thN >> 32);
+    iSb = dN.ip + dN.r0;
+    iSl = (dN.ok && !skip) ? dN.r1 - dN.r0 : 0u;
+    uint32_t nr = iSl == 0u ? 0u : ((iSb & 1u) + iSl + 127u) >> 7;
+    // no positive threshold: every tile of the band runs its epilogue (one
+    // row, possibly empty, in each tile)
+    if (PH == kRest && !th_pos && lt == 0u && (int)li < nx.bw) nr = max(nr, 1u);
+    iIncl = scan64(nr);
+    iExcl = iIncl - nr;
+    iTotal = lane_u32(iIncl, 63);
+    uint32_t R = max(iTotal, (uint32_t)kFR);
+    if ((R & 63u) != 0u && (R & 63u) < (uint32_t)kFR) R += (uint32_t)kFR - (R & 63u);
+    iR = R;
+    iJ0 = 0;
+    iSer = (iSer + 1u) & 0x3FFFFFFu;  // tags of consecutive items differ
+    ctxI.q = nx.q;
+    ctxI.b = nx.b;
+    ctxI.th = thN;
+    // prefetch: descriptors of the item after, terms of the one after that
+    BandCur nx3 = next(nx2);
+    dN = load_bdesc(nx2, tmN2);
+    thN = PH == kRest ? theta[nx2.q] : 0ull;
+    tmN2 = terms_of(nx3);
+    nx = nx2;
+    nx2 = nx3;
+  };
+
+  BandCur c0;
+  c0.rit = -1;
+  c0.end = 0;
+  c0.b = c0.q = 0;
+  c0.bw = 1;
+  nx = next(c0);
+  if (nx.rit >= ngi) return;
+  dN = load_bdesc(nx, terms_of(nx));
+  thN = PH == kRest ? theta[nx.q] : 0ull;
+  nx2 = next(nx);
+  tmN2 = terms_of(nx2);
+  for (int j = 0; j < D / 256; ++j)
+    reinterpret_cast<float4*>(acc)[j * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+  acc[D + lane] = 0.f;
+
+  // issue table: the chunk the next issued row comes from
+  bool items_left = true, iDead = false;
+  FlatTab tI;
+  uint32_t nI = 0, il = 0;
+  auto next_chunk = [&]() {  // tI <- the chunk after it (or the dead tail)
+    if (iJ0 + 64u < iR) {
+      iJ0 += 64u;
+    } else if (items_left && nx.rit < ngi) {
+      enter_item();
+    } else {
+      items_left = false;
+      iDead = true;
+      tI.base = 0u;
+      tI.off = 0u;
+      tI.len = 0u;
+      tI.sid = kDeadSid;
+      nI = 0x7FFFFFFFu;
+      il = 0;
+      return;
+    }
+    tI = flat_chunk(iSb, iSl, iIncl, iExcl, iTotal, iJ0, iSer);
+    nI = min(64u, iR - iJ0);
+    il = 0;
+  };
+  enter_item();
+  tI = flat_chunk(iSb, iSl, iIncl, iExcl, iTotal, 0u, iSer);
+  nI = min(64u, iR);
+  il = 0;
+
+  // ring: slot s holds the raw loads of rows r == s (mod kFR)
+  uint32_t ldR[kFR];
+  float v0R[kFR], v1R[kFR];
+  auto issue = [&](int s) {
+    if (il == nI) next_chunk();
+    const uint32_t base = lane_u32(tI.base, (int)il);
+    ldR[s] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)(lane * 4u), (int)(base * 2u), 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)(lane * 8u), (int)(base * 4u), 0);
+    v0R[s] = __uint_as_float((uint32_t)v[0]);
+    v1R[s] = __uint_as_float((uint32_t)v[1]);
+    ++il;
+  };
+#pragma unroll
+  for (int s = 0; s < kFR; ++s) issue(s);  // the first chunk holds >= kFR rows
+
+  // process side
+  FlatTab tP = tI;
+  uint32_t nP = nI, pl = 0;
+  FlatCtx ctxP = ctxI, ctxE = ctxI;
+  auto thf_of = [&](uint64_t th) -> float {
+    return (PH == kRest && a.nonneg && th_positive(th)) ? key_score((uint32_t)(th >> 32))
+                                                         : __builtin_nanf("");
+  };
+  float thfP = thf_of(ctxP.th);
+  uint32_t curTag = kNoTag;
+  uint64_t hit = 0;
+  bool done = false;
+
+  auto epilogue = [&]() {
+    const int32_t ti = ctxE.b * kBandW + (int32_t)(curTag & 7u);
+    const int64_t tile = tile_of32<PH>((uint32_t)ti, (uint32_t)P, (uint32_t)G);
+    if constexpr (PH == kRest) {
+      const bool flagged = a.nonneg && th_positive(ctxE.th);
+      if (flagged && hit == 0)
+        zero_acc<S>(acc);
+      else
+        emit_rest<S>(acc, tile, a.n_docs, ctxE.th, list + (int64_t)ctxE.q * C,
+                     list_cnt + ctxE.q, C);
+    } else {
+      best_dense<S, SM, true>(acc, tile, a.n_docs, (uint32_t)a.doc_offset,
+                              cand + (int64_t)ctxE.q * cstride + (int64_t)ti * SM);
+    }
+  };
+
+  // the current row (its slot already consumed): masked slots and scores,
+  // the accumulator values read one step early, its segment id
+  uint32_t sc0, sc1, sidC;
+  float ac0, ac1, xc0, xc1;
+  auto prepare = [&](int s) {  // row pl of tP, from slot s
+    sidC = lane_u32(tP.sid, (int)pl);
+    const uint32_t off = lane_u32(tP.off, (int)pl), len = lane_u32(tP.len, (int)pl);
+    const uint32_t p0 = off + 2u * lane;
+    const bool m0 = p0 < len, m1 = p0 + 1u < len;
+    sc0 = m0 ? (ldR[s] & 0xFFFFu) : trash;
+    sc1 = m1 ? (ldR[s] >> 16) : trash;
+    ac0 = m0 ? v0R[s] : 0.f;
+    ac1 = m1 ? v1R[s] : 0.f;
+    xc0 = acc[sc0];
+    xc1 = acc[sc1];
+  };
+  prepare(0);
+
+  // step of ring slot s: row r (prepared) is added, row r + kFR goes into slot
+  // s (consumed by the previous step), row r + 1 is prepared from slot s + 1
+  auto step = [&](int s) {
+    issue(s);
+    if (sidC != kDeadSid) {
+      const uint32_t tag = sidC >> 3;
+      if (tag != curTag) {
+        if (curTag != kNoTag) epilogue();
+        hit = 0;
+        curTag = tag;
+        ctxE = ctxP;
+        xc0 = 0.f;  // read before the epilogue cleared the accumulator
+        xc1 = 0.f;
+      }
+    }
+    const float y0 = xc0 + ac0, y1 = xc1 + ac1;
+    acc[sc0] = y0;
+    acc[sc1] = y1;
+    if (PH == kRest) hit |= __ballot(y0 >= thfP) | __ballot(y1 >= thfP);
+    if (++pl == nP) {  // the process side enters the issue side's chunk
+      tP = tI;
+      nP = nI;
+      pl = 0;
+      ctxP = ctxI;
+      thfP = thf_of(ctxP.th);
+      done = iDead;
+    }
+    prepare((s + 1) % kFR);
+  };
+
+  while (!done) {
+#pragma unroll
+    for (int s = 0; s < kFR; ++s) step(s);
+  }
+  if (curTag != kNoTag) epilogue();
+}
+
 // ---------------------------------------------------------------------------
 // Exact top-k of each flagged tile (persistent, queue-driven; every wave
 // reaches the exit test each iteration).  Wave 0 accumulates the tile; the
@@ -2358,6 +2712,12 @@ static bool use_band(const DevIndex& ix, int64_t T) {
   return !off && T >= 1 && T <= kBandT && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
 }
 
+// The flat kernel replaces the band kernel's tile loop (BM25_FLAT=0: band).
+static bool use_flat() {
+  static const bool off = getenv("BM25_FLAT") && atoi(getenv("BM25_FLAT")) == 0;
+  return !off;
+}
+
 template <int S, int PH, int SM = 1>
 static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
                         const Workspace& ws, hipStream_t st) {
@@ -2377,6 +2737,22 @@ static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const S
   const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kBandW;
   IndexArgs a = args_of(ix);
   a.seg = ws.seg;
+  if (use_flat()) {
+#define BM25_FLAT_LAUNCH(SPV)                                                                     \
+  {                                                                                               \
+    const int grid = persistent_grid<S, PH>(score_flat_kernel<S, PH, SM, SPV>, 64);               \
+    hipLaunchKernelGGL((score_flat_kernel<S, PH, SM, SPV>), dim3((unsigned)grid), dim3(64), 0, st, \
+                       a, q, (int32_t)T, sg.P, sg.G, sg.nq_host, ws.theta, sg.cand_out,           \
+                       sg.cstride, ws.list, ws.list_cnt, ws.list_cap, ws.wctr, band_claim(),      \
+                       claim_m(), skip ? sg.sample_keys : nullptr, sg.sample_stride);             \
+  }
+    if (ix.sparse)
+      BM25_FLAT_LAUNCH(true)
+    else
+      BM25_FLAT_LAUNCH(false)
+#undef BM25_FLAT_LAUNCH
+    return;
+  }
   if (ix.sparse) {
     const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM, true>, 64 * kBandWaves);
     hipLaunchKernelGGL((score_band_kernel<S, PH, SM, true>), dim3((unsigned)grid),

@@ -359,6 +359,30 @@ def test_bm25_dense_model_golden(gpu):
                 assert have == want, (q, v, have, want)
 
 
+def test_bm25_top_n_past_kmaxk(gpu):
+    """get_top_n with n > kMaxK (4096) ranks every document like the
+    reference's argsort (bm25.py:172-178): same (score, doc) pairs as the
+    engine's own top-k where they overlap, scores non-increasing, ties by
+    index ascending."""
+    import bm25
+    rng = np.random.default_rng(7)
+    words = [f"w{i}" for i in range(60)]
+    corpus = [list(rng.choice(words, size=int(rng.integers(3, 12)))) for _ in range(5000)]
+    m = bm25.BM25()
+    m.fit(corpus)
+    q = ["w1", "w7", "w30", "w59"]
+    full = m.get_top_n(q, corpus, n=4500)
+    assert len(full) == 4500
+    sc = np.array([t[0] for t in full])
+    assert np.all(np.diff(sc) <= 0)
+    top = m.get_top_n(q, corpus, n=100)
+    assert [t[0] for t in top] == list(sc[:100])
+    assert [t[1] for t in top] == [t[1] for t in full[:100]]
+    dense = m.get_scores(q).astype(np.float32)
+    order = np.lexsort((np.arange(len(corpus)), -dense))[:4500]
+    assert [corpus[i] for i in order] == [t[1] for t in full]
+
+
 def test_bm25s_directory_drop_in(gpu, tmp_path):
     """BM25v.from_bm25s over a bm25s index directory (the animal fixture written
     back to disk): the bm25_test.py:23 query returns the reference's golden."""
