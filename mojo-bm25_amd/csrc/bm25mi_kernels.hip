@@ -883,6 +883,44 @@ __device__ __forceinline__ void best_dense(float* acc, int64_t tile, int64_t n_d
   }
 }
 
+// One key per tile, positive sums only (the flat kernel's SAMPLE epilogue):
+// the tile's best score by a float max over each lane's entries (sums >= 0
+// compare as their bit patterns), then the smallest doc holding it from a
+// second read; the accumulators are cleared.  Same key as best_dense<S, 1,
+// true>, about half its VALU work.
+template <int S>
+__device__ __forceinline__ void best1_pos(float* acc, int64_t tile, uint32_t idoff,
+                                          uint64_t* __restrict__ out) {
+  constexpr int E4 = (1 << S) / 256;  // float4 groups per lane
+  float4* a4 = reinterpret_cast<float4*>(acc);
+  const uint32_t lane = lane_id();
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < E4; ++j) {
+    const float4 f = a4[j * 64 + lane];
+    m = fmaxf(m, fmaxf(fmaxf(f.x, f.y), fmaxf(f.z, f.w)));
+  }
+  const uint32_t wm = wave_max_u32(__float_as_uint(m));
+  uint64_t key = 0ull;
+  if (wm != 0u) {
+    const float fm = __uint_as_float(wm);
+    uint32_t bd = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = E4 - 1; j >= 0; --j) {  // last match written = smallest doc
+      const float4 f = a4[j * 64 + lane];
+      bd = f.w == fm ? entry_doc(4 * j + 3, lane) : bd;
+      bd = f.z == fm ? entry_doc(4 * j + 2, lane) : bd;
+      bd = f.y == fm ? entry_doc(4 * j + 1, lane) : bd;
+      bd = f.x == fm ? entry_doc(4 * j + 0, lane) : bd;
+    }
+    const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(0xFFFFFFFFu - bd);
+    key = ((uint64_t)score_key(fm) << 32) |
+          (uint64_t)(0xFFFFFFFFu - (uint32_t)((tile << S) + doc) - idoff);
+  }
+  zero_acc<S>(acc);
+  if (lane == 0) *out = key;
+}
+
 // Item of the pipelined kernel: XCD-relative ordinal rit (end = its chunk's
 // end), phase tile ti = the tib-th tile of a band of bw tiles, query qi, and
 // the tile it scores.
@@ -1729,7 +1767,12 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
 // (ablation: 2.49 of its 4.35 ms with no loads, adds or emission) is what
 // this removes.  Each doc's adds stay in query-term order (bm25_native.py:152).
 // ===========================================================================
-constexpr int kFR = 4;                       // rows in flight (ring slots)
+#ifndef BM25_FR    // rows in flight (ring slots): REST, SAMPLE
+#define BM25_FR 10
+#endif
+#ifndef BM25_FR_S
+#define BM25_FR_S 10
+#endif
 constexpr uint32_t kDeadSid = 0xFFFFFFFFu;   // padding row: no adds, no tile
 constexpr uint32_t kNoTag = 0xFFFFFFFFu;     // accumulator holds no tile
 
@@ -1750,8 +1793,7 @@ __device__ __forceinline__ uint32_t scan64(uint32_t x) {
 
 struct FlatTab {    // one chunk of an item's rows: lane r = row j0 + r
   uint32_t base;    // even posting index of the row's first pair (0: dead row)
-  uint32_t off;     // base - segment start: lane l holds segment postings off + 2l, off + 2l + 1
-  uint32_t len;     // segment length (0: every lane masked)
+  uint32_t pk;      // valid postings [lo, hi) of the row's 128 (lo = pk & 1, hi = pk >> 1)
   uint32_t sid;     // (item serial << 6) | tile * 8 + term; kDeadSid: padding
 };
 
@@ -1778,9 +1820,12 @@ __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t
   const uint32_t l = (uint32_t)__shfl((int)sl, pos, 64);
   const bool in = j < total;
   FlatTab t;
-  t.base = (in && l != 0u) ? (b & ~1u) + 128u * (j - e) : 0u;
-  t.off = t.base - b;
-  t.len = in ? l : 0u;
+  const uint32_t k = j - e;  // row of its segment
+  t.base = (in && l != 0u) ? (b & ~1u) + 128u * k : 0u;
+  // row positions p of the segment: p + base in [b, b + l)
+  const uint32_t rlo = k == 0u ? (b & 1u) : 0u;
+  const uint32_t rhi = min(128u, (b & 1u) + l - 128u * k);
+  t.pk = (in && l != 0u) ? (rlo | (rhi << 1)) : 1u;
   t.sid = in ? (ser << 6) | (uint32_t)pos : kDeadSid;
   return t;
 }
@@ -1793,6 +1838,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
     const uint64_t* __restrict__ skeys, int64_t sstride) {
   constexpr int D = 1 << S;
+  constexpr int kFR = PH == kSample ? BM25_FR_S : BM25_FR;  // ring slots (>= 2)
   __shared__ __attribute__((aligned(16))) float acc[D + 64];
   const uint32_t lane = lane_id();
   const uint32_t trash = (uint32_t)D + lane;  // this lane's always-zero slot
@@ -1944,8 +1990,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       items_left = false;
       iDead = true;
       tI.base = 0u;
-      tI.off = 0u;
-      tI.len = 0u;
+      tI.pk = 1u;
       tI.sid = kDeadSid;
       nI = 0x7FFFFFFFu;
       il = 0;
@@ -1976,7 +2021,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   for (int s = 0; s < kFR; ++s) issue(s);  // the first chunk holds >= kFR rows
 
   // process side
-  FlatTab tP = tI;
+  uint32_t tPpk = tI.pk, tPsid = tI.sid;  // the process side's chunk (no bases)
   uint32_t nP = nI, pl = 0;
   FlatCtx ctxP = ctxI, ctxE = ctxI;
   auto thf_of = [&](uint64_t th) -> float {
@@ -1999,8 +2044,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
         emit_rest<S>(acc, tile, a.n_docs, ctxE.th, list + (int64_t)ctxE.q * C,
                      list_cnt + ctxE.q, C);
     } else {
-      best_dense<S, SM, true>(acc, tile, a.n_docs, (uint32_t)a.doc_offset,
-                              cand + (int64_t)ctxE.q * cstride + (int64_t)ti * SM);
+      uint64_t* out = cand + (int64_t)ctxE.q * cstride + (int64_t)ti * SM;
+      if constexpr (SM == 1)
+        best1_pos<S>(acc, tile, (uint32_t)a.doc_offset, out);
+      else
+        best_dense<S, SM, true>(acc, tile, a.n_docs, (uint32_t)a.doc_offset, out);
     }
   };
 
@@ -2008,11 +2056,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // the accumulator values read one step early, its segment id
   uint32_t sc0, sc1, sidC;
   float ac0, ac1, xc0, xc1;
-  auto prepare = [&](int s) {  // row pl of tP, from slot s
-    sidC = lane_u32(tP.sid, (int)pl);
-    const uint32_t off = lane_u32(tP.off, (int)pl), len = lane_u32(tP.len, (int)pl);
-    const uint32_t p0 = off + 2u * lane;
-    const bool m0 = p0 < len, m1 = p0 + 1u < len;
+  auto prepare = [&](int s) {  // row pl of the process chunk, from slot s
+    sidC = lane_u32(tPsid, (int)pl);
+    const uint32_t pk = lane_u32(tPpk, (int)pl);
+    const uint32_t p0 = 2u * lane, rhi = pk >> 1;
+    const bool m0 = p0 >= (pk & 1u) && p0 < rhi, m1 = p0 + 1u < rhi;
     sc0 = m0 ? (ldR[s] & 0xFFFFu) : trash;
     sc1 = m1 ? (ldR[s] >> 16) : trash;
     ac0 = m0 ? v0R[s] : 0.f;
@@ -2040,9 +2088,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const float y0 = xc0 + ac0, y1 = xc1 + ac1;
     acc[sc0] = y0;
     acc[sc1] = y1;
-    if (PH == kRest) hit |= __ballot(y0 >= thfP) | __ballot(y1 >= thfP);
+    if (PH == kRest) hit |= __ballot(fmaxf(y0, y1) >= thfP);
     if (++pl == nP) {  // the process side enters the issue side's chunk
-      tP = tI;
+      tPpk = tI.pk;
+      tPsid = tI.sid;
       nP = nI;
       pl = 0;
       ctxP = ctxI;

@@ -4,7 +4,7 @@
 # Outputs under gpurun_out/r02prof/.  Each step has its own time limit.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/r02prof
+OUT=$R/gpurun_out/${PROF_NAME:-r02prof}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
@@ -14,7 +14,7 @@ i=0
 while read -r ctrs; do
   [ -z "$ctrs" ] && continue
   i=$((i+1))
-  timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-include-regex "score_band" --output-format csv -d $OUT/pmc_p$i -o pmc -- python3 $R/scripts/ablate.py ${CFG:-c3} > $OUT/pmc_p$i.log 2>&1 || { echo pmc pass $i failed; tail -5 $OUT/pmc_p$i.log; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-include-regex "score_(band|flat)" --output-format csv -d $OUT/pmc_p$i -o pmc -- python3 $R/scripts/ablate.py ${CFG:-c3} > $OUT/pmc_p$i.log 2>&1 || { echo pmc pass $i failed; tail -5 $OUT/pmc_p$i.log; exit 1; }
 done <<'CTRS'
 TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum
 WRITE_SIZE
