@@ -109,12 +109,24 @@ int bm25_search(bm25_index* idx, const int32_t* queries, int64_t Q, int64_t T,
 /*
  * Same as bm25_search with device-resident queries and results, enqueued on
  * `stream` without host synchronisation (the bench's timed step: inputs
- * already resident in HBM).  Token ids are NOT validated on the host here:
- * ids >= n_terms are treated as padding by the kernels.
+ * already resident in HBM).  Token ids are NOT validated here: ids >=
+ * n_terms are treated as padding by the kernels (bm25_max_token_device is
+ * the opt-in check).
  */
 int bm25_search_device(bm25_index* idx, const int32_t* d_queries, int64_t Q,
                        int64_t T, int32_t k, int32_t* d_docs, float* d_scores,
                        void* stream);
+
+/*
+ * Opt-in validation of a device-resident batch: *max_token = the largest
+ * token id of d_queries[Q, T] (0 when none is positive), computed on the
+ * device on `stream`, which is synchronised.  A caller of bm25_search_device
+ * that wants the reference's check raises when *max_token >= n_terms.
+ * Replaces: bm25_native.py:91-96 (queries.max(initial=0) >= n_terms ->
+ *           ValueError).
+ */
+int bm25_max_token_device(bm25_index* idx, const int32_t* d_queries, int64_t Q,
+                          int64_t T, int32_t* max_token, void* stream);
 
 /*
  * GPU index build: (doc, term, tf) triples + document lengths -> the CSC

@@ -54,6 +54,7 @@ _SIGS = {
     "bm25_index_segments": ([_P, _PI32, _PI64], ctypes.c_int),
     "bm25_search": ([_P, _P, _I64, _I64, _I32, _P, _P], ctypes.c_int),
     "bm25_search_device": ([_P, _P, _I64, _I64, _I32, _P, _P, _P], ctypes.c_int),
+    "bm25_max_token_device": ([_P, _P, _I64, _I64, _P, _P], ctypes.c_int),
     "bm25_scores_dense": ([_P, _P, _I64, _P], ctypes.c_int),
     "bm25_merge_topk_device": ([ctypes.c_int, _P, _P, _I64, _I64, _I32, _P, _P, _P],
                                ctypes.c_int),

@@ -106,11 +106,29 @@ class GpuIndex:
         check(lib.bm25_search(self._h, _ptr(q), Q, T, k, _ptr(docs), _ptr(scores)))
         return docs, scores
 
-    def search_device(self, d_queries, k: int, d_docs, d_scores, stream=None) -> None:
-        """Device-resident search: torch int32 [Q, T] in, int32/f32 [Q, k] out,
-        enqueued on ``stream`` (a torch.cuda.Stream or raw handle)."""
+    def max_token_device(self, d_queries, stream=None) -> int:
+        """Largest token id of a device batch (bm25_max_token_device; syncs)."""
         Q, T = d_queries.shape
         s = getattr(stream, "cuda_stream", stream) or 0
+        m = ctypes.c_int32()
+        check(lib.bm25_max_token_device(self._h, ctypes.c_void_p(d_queries.data_ptr()), Q, T,
+                                        ctypes.byref(m), ctypes.c_void_p(s)))
+        return m.value
+
+    def search_device(self, d_queries, k: int, d_docs, d_scores, stream=None,
+                      validate: bool = False) -> None:
+        """Device-resident search: torch int32 [Q, T] in, int32/f32 [Q, k] out,
+        enqueued on ``stream`` (a torch.cuda.Stream or raw handle).  Token ids
+        >= n_terms count as padding unless ``validate`` (a synchronising
+        device check) raises the reference's ValueError (bm25_native.py:91-96)."""
+        Q, T = d_queries.shape
+        s = getattr(stream, "cuda_stream", stream) or 0
+        if validate:
+            m = self.max_token_device(d_queries, stream)
+            if m >= self.n_terms:
+                raise ValueError(
+                    f"The maximum token ID in the query ({m}) is higher than the number "
+                    "of tokens in the index.")
         check(lib.bm25_search_device(self._h, ctypes.c_void_p(d_queries.data_ptr()), Q, T,
                                      int(k), ctypes.c_void_p(d_docs.data_ptr()),
                                      ctypes.c_void_p(d_scores.data_ptr()), ctypes.c_void_p(s)))

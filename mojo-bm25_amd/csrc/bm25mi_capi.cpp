@@ -76,6 +76,7 @@ struct bm25_index {
   EventPair* split_ev = nullptr;  // events of a sample/finish search in flight
   hipEvent_t ws_done = nullptr;    // end of the last search that used the workspace
   hipStream_t ws_stream = nullptr; // its stream
+  int32_t* d_maxtok = nullptr;     // bm25_max_token_device result
 };
 
 namespace {
@@ -330,14 +331,20 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
   } while (0)
   TRYC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
   // segment table form (DevIndex): BM25_SEGMENTS=dense|sparse; by default the
-  // dense V x (ntiles+1) table unless it would outgrow twice the posting
-  // arrays (6 B per posting) — then the O(pairs) tile lists
+  // dense V x (ntiles+1) table (O(1) lookups, no per-search table: config 5's
+  // 24 GB per rank ran 6 % faster than the tile lists) unless it would
+  // outgrow both twice the posting arrays (6 B per posting) and 1/8 of the
+  // device's memory — then the O(pairs) tile lists
   const int64_t rel_elems = n_terms * (ntiles + 1);
   {
     const char* m = getenv("BM25_SEGMENTS");
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) total_b = 0;
+    const int64_t rel_bytes = rel_elems * 4;
     if (m && !strcmp(m, "sparse")) ix.sparse = true;
     else if (m && !strcmp(m, "dense")) ix.sparse = false;
-    else ix.sparse = rel_elems * 4 > 2 * 6 * std::max<int64_t>(nnz, 1);
+    else ix.sparse = rel_bytes > 2 * 6 * std::max<int64_t>(nnz, 1) &&
+                     rel_bytes > (int64_t)(total_b / 8);
   }
   TRYC(hipMalloc(&ix.indptr, sizeof(int64_t) * (n_terms + 1)), "hipMalloc(indptr)");
   if (!ix.sparse)
@@ -414,6 +421,7 @@ int bm25_index_destroy(bm25_index* h) {
   hipFree(h->d_q);
   hipFree(h->d_docs);
   hipFree(h->d_scores);
+  hipFree(h->d_maxtok);
   hipFree(h->ix.indptr);
   hipFree(h->ix.rel);
   hipFree(h->ix.tl_ptr);
@@ -486,6 +494,21 @@ int bm25_search_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
   return run_search(h, d_queries, Q, T, k, d_docs, d_scores, (hipStream_t)stream);
+}
+
+int bm25_max_token_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T,
+                          int32_t* max_token, void* stream) {
+  if (!h || !max_token) return fail(BM25_EINVAL, "NULL argument");
+  if (Q < 0 || T < 0) return fail(BM25_EINVAL, "negative query shape");
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  if (!h->d_maxtok) HIP_TRY(hipMalloc(&h->d_maxtok, sizeof(int32_t)), "hipMalloc");
+  const hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(launch_max_token(d_queries, Q * T, h->d_maxtok, st), "max_token_kernel");
+  HIP_TRY(hipMemcpyAsync(max_token, h->d_maxtok, sizeof(int32_t), hipMemcpyDeviceToHost, st),
+          "hipMemcpyAsync");
+  HIP_TRY(hipStreamSynchronize(st), "hipStreamSynchronize");
+  return BM25_OK;
 }
 
 // Two-phase search of W doc shards with a global threshold (bm25mi.h).

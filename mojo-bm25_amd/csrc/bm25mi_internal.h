@@ -156,6 +156,10 @@ hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores,
                               int64_t W, int64_t Q, int k, int32_t* d_out_docs,
                               float* d_out_scores, hipStream_t stream);
 
+// Largest token id of [n] device ids (0 if none is positive) into *d_out.
+hipError_t launch_max_token(const int32_t* d_queries, int64_t n, int32_t* d_out,
+                            hipStream_t stream);
+
 // Tile shifts with compiled kernels.
 bool tile_shift_supported(int s);
 

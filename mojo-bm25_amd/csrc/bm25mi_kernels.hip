@@ -2848,6 +2848,28 @@ __global__ __launch_bounds__(256) void seg_table_kernel(IndexArgs a,
   }
 }
 
+// Largest token id of a device-resident query batch (bm25_native.py:91,
+// queries.max(initial=0)), for the opt-in check of bm25_max_token_device.
+__global__ __launch_bounds__(256) void max_token_kernel(const int32_t* __restrict__ q, int64_t n,
+                                                        int32_t* __restrict__ out) {
+  int32_t m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    m = max(m, q[i]);
+  m = (int32_t)wave_max_u32((uint32_t)max(m, 0));  // ids >= 0 compare as unsigned
+  if (lane_id() == 0 && m > 0) atomicMax(out, m);
+}
+
+hipError_t launch_max_token(const int32_t* d_queries, int64_t n, int32_t* d_out,
+                            hipStream_t stream) {
+  hipMemsetAsync(d_out, 0, sizeof(int32_t), stream);
+  if (n > 0) {
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(max_token_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d_queries,
+                       n, d_out);
+  }
+  return hipGetLastError();
+}
+
 int64_t seg_entries(const DevIndex& ix, int64_t Q) {
   return ix.sparse ? Q * ((ix.ntiles + 7) >> 3) * 64 : 0;
 }

@@ -220,6 +220,30 @@ def test_search_device_torch(gpu):
            oracle.search_c(n, g["indptr"], g["indices"], g["data"], g["queries"], 10))
 
 
+def test_search_device_opt_in_validation(gpu):
+    """bm25_max_token_device: the reference's max-token check
+    (bm25_native.py:91-96) on a device batch; search_device(validate=True)
+    raises its ValueError, the default treats the id as padding."""
+    import torch
+    g = _load("synth_small.npz")
+    n = int(g["n_docs"])
+    ix = _idx(g["indptr"], g["indices"], g["data"], n)
+    q = g["queries"].copy()
+    assert ix.max_token_device(torch.from_numpy(q).to("cuda:0")) == int(q.max(initial=0))
+    assert ix.max_token_device(torch.full((3, 4), -1, dtype=torch.int32, device="cuda:0")) == 0
+    q[1, 0] = ix.n_terms + 5
+    dq = torch.from_numpy(q).to("cuda:0")
+    dd = torch.empty((q.shape[0], 10), dtype=torch.int32, device="cuda:0")
+    ds = torch.empty((q.shape[0], 10), dtype=torch.float32, device="cuda:0")
+    with pytest.raises(ValueError, match=r"maximum token ID in the query \(%d\)" % (ix.n_terms + 5)):
+        ix.search_device(dq, 10, dd, ds, validate=True)
+    ix.search_device(dq, 10, dd, ds)  # unchecked: the id is padding
+    torch.cuda.synchronize()
+    q[1, 0] = -1
+    _exact((dd.cpu().numpy(), ds.cpu().numpy()),
+           oracle.search_c(n, g["indptr"], g["indices"], g["data"], q, 10))
+
+
 def test_sharded_merge_equals_single_index(gpu):
     import torch
     from bm25mi import synth
@@ -287,6 +311,7 @@ def test_config3_full_batch_parity(gpu):
     {"BM25_SEGMENTS": "sparse"}, {"BM25_SEGMENTS": "sparse", "BM25_SAMPLE_P": "1"},
     {"BM25_SEGMENTS": "sparse", "BM25_NO_BAND": "1"},
     {"BM25_SEGMENTS": "sparse", "BM25_LIST_CAP": "8", "BM25_TILE_SHIFT": "10"},
+    {"BM25_FLAT": "0"}, {"BM25_FLAT": "0", "BM25_SEGMENTS": "sparse"},
 ])
 def test_kernel_variants_bit_exact(gpu, variant, monkeypatch):
     """Every search configuration gives the oracle's bits: sampling strides
@@ -641,11 +666,11 @@ def test_config3_sparse_segments_full_batch(gpu, monkeypatch):
 def test_config5_shape_int64_shards_sparse(gpu, tmp_path, monkeypatch):
     """Config 5 in miniature: a collection written as a bm25s directory with
     an int64 indptr, cut per rank by bm25mi.shard (streamed column blocks),
-    each rank's shard on the sparse segment table (chosen automatically:
-    its vocabulary is large for its tile count), searched with the global
+    each rank's shard on the sparse segment table, searched with the global
     threshold protocol and merged — bit-exact vs the oracle on the whole
     collection."""
     import torch
+    monkeypatch.setenv("BM25_SEGMENTS", "sparse")
     from bm25mi import synth
     from bm25mi.bm25s_io import save_bm25s
     from bm25mi.shard import load_bm25s_shard
@@ -662,7 +687,7 @@ def test_config5_shape_int64_shards_sparse(gpu, tmp_path, monkeypatch):
     for r in range(W):
         sip, six, sdt, n, lo, _ = load_bm25s_shard(str(tmp_path), r, W)
         sh = GpuIndex(sip, six, sdt, n, doc_offset=lo)
-        assert sh.info()["sparse"]  # chosen automatically (V x ntiles > 2x postings)
+        assert sh.info()["sparse"]
         shards.append(sh)
         sdm = max(sdm, n)
     ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k, threads=16)
