@@ -1836,14 +1836,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int64_t cstride,
     uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
     int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
-    const uint64_t* __restrict__ skeys, int64_t sstride) {
+    const uint64_t* __restrict__ skeys, int64_t sstride, int32_t BW) {
   constexpr int D = 1 << S;
   constexpr int kFR = PH == kSample ? BM25_FR_S : BM25_FR;  // ring slots (>= 2)
   __shared__ __attribute__((aligned(16))) float acc[D + 64];
   const uint32_t lane = lane_id();
   const uint32_t trash = (uint32_t)D + lane;  // this lane's always-zero slot
   const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
-  const int32_t nb = (nt + kBandW - 1) / kBandW;
+  const int32_t nb = (nt + BW - 1) / BW;  // items: (query, BW <= 8 consecutive phase tiles)
   const int64_t nitems = (int64_t)nb * nq;
   const int64_t per = (nitems + 7) >> 3;
   const int grp = (int)(blockIdx.x & 7);
@@ -1870,7 +1870,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       if (++c.q == nq) {
         c.q = 0;
         ++c.b;
-        c.bw = min(kBandW, nt - c.b * kBandW);
+        c.bw = min(BW, nt - c.b * BW);
       }
       return c;
     }
@@ -1886,19 +1886,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const uint32_t it = lo + (uint32_t)bb;
     n.b = (int32_t)(it / (uint32_t)nq);
     n.q = (int32_t)(it - (uint32_t)n.b * (uint32_t)nq);
-    n.bw = min(kBandW, nt - n.b * kBandW);
+    n.bw = min(BW, nt - n.b * BW);
     return n;
   };
   auto terms_of = [&](const BandCur& c) -> int32_t {
     return queries[(int64_t)c.q * T + (int)min(lt, (uint32_t)(T - 1))];
   };
-  const bool skipping = PH == kRest && skeys != nullptr && G == kBandW;
+  // REST: sample tiles (groups of G = kSampleGroup tiles, one group per G * P)
+  // whose best sample key is below theta are skipped
+  const bool skipping = PH == kRest && skeys != nullptr && G == kSampleGroup;
   auto load_bdesc = [&](const BandCur& c, int32_t tm) -> BandDesc {
     BandDesc d;
     const int32_t term = __shfl(tm, (int)lt, 64);
     const bool ok = (int)lt < T && (int)li < c.bw && term >= 0 && term < a.V;
     const int64_t tt = ok ? term : 0;
-    const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b * kBandW + li), (uint32_t)P,
+    const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b * BW + li), (uint32_t)P,
                                                       (uint32_t)G)
                             : 0;
     if constexpr (SP) {
@@ -1914,9 +1916,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       d.r1 = r[1];
     }
     d.ok = ok ? 1u : 0u;
-    const int64_t si = (int64_t)(c.b / P) * kBandW + min(li, (uint32_t)(c.bw - 1));
-    d.skey = skipping ? skeys[(int64_t)c.q * sstride + min<int64_t>(si, sstride - 1)] : ~0ull;
-    if (!(skipping && (c.b % P) == 0)) d.skey = ~0ull;
+    const bool smp = skipping && ok && ((tile / G) % P) == 0;
+    const int64_t si = (tile / ((int64_t)G * P)) * G + tile % G;
+    d.skey = smp ? skeys[(int64_t)c.q * sstride + min<int64_t>(si, sstride - 1)] : ~0ull;
     return d;
   };
   auto th_positive = [&](uint64_t th) -> bool {
@@ -2034,7 +2036,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   bool done = false;
 
   auto epilogue = [&]() {
-    const int32_t ti = ctxE.b * kBandW + (int32_t)(curTag & 7u);
+    const int32_t ti = ctxE.b * BW + (int32_t)(curTag & 7u);
     const int64_t tile = tile_of32<PH>((uint32_t)ti, (uint32_t)P, (uint32_t)G);
     if constexpr (PH == kRest) {
       const bool flagged = a.nonneg && th_positive(ctxE.th);
@@ -2767,6 +2769,19 @@ static bool use_flat() {
   return !off;
 }
 
+// Tiles per flat-kernel item: 8, halved while the phase would give the
+// resident waves fewer than BM25_ITEMS_PER_WAVE (24) items each — a small doc
+// shard's SAMPLE pass has ~2 eight-tile items per wave, and the last wave's
+// items set the pass time (BM25_FLAT_BW forces a width).
+static int32_t flat_band(int64_t nt, int64_t nq, int grid) {
+  static const int forced = getenv("BM25_FLAT_BW") ? atoi(getenv("BM25_FLAT_BW")) : 0;
+  if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
+  static const int64_t per = getenv("BM25_ITEMS_PER_WAVE") ? atoi(getenv("BM25_ITEMS_PER_WAVE")) : 24;
+  int32_t bw = 8;
+  while (bw > 1 && ((nt + bw - 1) / bw) * nq < per * (int64_t)grid) bw >>= 1;
+  return bw;
+}
+
 template <int S, int PH, int SM = 1>
 static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
                         const Workspace& ws, hipStream_t st) {
@@ -2790,10 +2805,12 @@ static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const S
 #define BM25_FLAT_LAUNCH(SPV)                                                                     \
   {                                                                                               \
     const int grid = persistent_grid<S, PH>(score_flat_kernel<S, PH, SM, SPV>, 64);               \
+    const int64_t nt = PH == kSample ? sample_count(ix.ntiles, sg.P, sg.G) : ix.ntiles;          \
     hipLaunchKernelGGL((score_flat_kernel<S, PH, SM, SPV>), dim3((unsigned)grid), dim3(64), 0, st, \
                        a, q, (int32_t)T, sg.P, sg.G, sg.nq_host, ws.theta, sg.cand_out,           \
                        sg.cstride, ws.list, ws.list_cnt, ws.list_cap, ws.wctr, band_claim(),      \
-                       claim_m(), skip ? sg.sample_keys : nullptr, sg.sample_stride);             \
+                       claim_m(), skip ? sg.sample_keys : nullptr, sg.sample_stride,              \
+                       flat_band(nt, sg.nq_host, grid));                                          \
   }
     if (ix.sparse)
       BM25_FLAT_LAUNCH(true)

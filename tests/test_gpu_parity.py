@@ -312,6 +312,8 @@ def test_config3_full_batch_parity(gpu):
     {"BM25_SEGMENTS": "sparse", "BM25_NO_BAND": "1"},
     {"BM25_SEGMENTS": "sparse", "BM25_LIST_CAP": "8", "BM25_TILE_SHIFT": "10"},
     {"BM25_FLAT": "0"}, {"BM25_FLAT": "0", "BM25_SEGMENTS": "sparse"},
+    {"BM25_FLAT_BW": "1"}, {"BM25_FLAT_BW": "2", "BM25_SEGMENTS": "sparse"},
+    {"BM25_FLAT_BW": "4", "BM25_SAMPLE_P": "2"},
 ])
 def test_kernel_variants_bit_exact(gpu, variant, monkeypatch):
     """Every search configuration gives the oracle's bits: sampling strides
