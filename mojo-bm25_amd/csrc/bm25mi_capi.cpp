@@ -127,7 +127,7 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
   HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
   HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * 4), "hipMemset(counters)");
-  HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrInts), "hipMalloc(wctr)");
+  HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMalloc(wctr)");
   ws.cap_seg = seg_entries(h->ix, q);
   if (ws.cap_seg > 0) HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * ws.cap_seg), "hipMalloc(seg)");
   ws.list_cap = C;

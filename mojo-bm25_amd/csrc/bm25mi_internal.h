@@ -60,6 +60,8 @@ constexpr int kBand = 8;
 #endif
 constexpr int kSampleGroup = BM25_BANDW;
 constexpr int kWctrInts = 8 * kClaimM * kCtrStride;
+// Claim-counter regions of a search: SAMPLE, REST (or the exact pass), fallback.
+constexpr int kWctrRegions = 3;
 
 struct DevIndex {
   int device = 0;
@@ -98,7 +100,7 @@ struct Workspace {
   int32_t* queue = nullptr;      // [Q*maxflag] items = qi*maxflag + i
   int32_t* counters = nullptr;   // [0]/[1] rescore queue length / pop cursor,
                                  // [2] fallback queries, [3] tiles re-scored this search
-  int32_t* wctr = nullptr;       // [kWctrInts] item-claim counters, zeroed before each score launch
+  int32_t* wctr = nullptr;       // [kWctrRegions][kWctrInts] item-claim counters, zeroed per search
   uint64_t* seg = nullptr;       // sparse index: [Q][bands][64] segment of (tile, term) lanes of
                                  // each band item (start | len << 32), built per search
   int64_t cap_seg = 0;           // u64 entries of seg

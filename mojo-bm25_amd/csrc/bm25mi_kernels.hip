@@ -121,6 +121,8 @@ struct Stage {
   int32_t nq_host;           // stage queries (host bound)
   int32_t* fb;               // overflowed queries are appended here
   int32_t* fb_cnt;
+  int32_t ctr_region;        // claim counters of the launch: ws.wctr + region * kWctrInts
+  bool ctr_zeroed;           // ... already zeroed by the search's zero_search_kernel
 };
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -145,6 +147,16 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
   const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
   return max(max(a, b), max(c, d));
+}
+
+// Sum over the 64 lanes of a wave (DPP inside 16-lane rows, then SGPRs).
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
 // Inclusive prefix sum over the wave.
@@ -819,7 +831,7 @@ __device__ __forceinline__ void best_sparse(float* acc, const uint32_t (&l0)[kJ]
       bk[i] = better ? key : bk[i];
     }
   }
-  const uint32_t base = (uint32_t)(tile << S) + idoff;  // global doc ids (theta_kernel)
+  const uint32_t base = (uint32_t)(tile << S) + idoff;  // global doc ids (theta_wave_kernel)
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     const uint32_t wm = wave_max_u32(bk[i]);
@@ -2446,14 +2458,6 @@ constexpr uint64_t kZeroFillTheta = (uint64_t)0x80800000u << 32;
 // positive sum) gets kZeroFillTheta on a non-negative index; otherwise it gets
 // no threshold: theta = all ones (a NaN score: no REST key passes) and its list
 // is marked overflowed, which sends it to the exact fallback stage.
-struct SrcShards {  // query q's sample keys of W shards: [W][Q][S]
-  const uint64_t* keys;
-  int64_t Q, S, q;
-  __device__ uint64_t operator()(int64_t i) const {
-    const int64_t w = i / S;
-    return keys[(w * Q + q) * S + (i - w * S)];
-  }
-};
 
 //
 // Sample keys carry GLOBAL doc ids (doc_offset + local), so the k-th key is
@@ -2461,17 +2465,62 @@ struct SrcShards {  // query q's sample keys of W shards: [W][Q][S]
 // score, tie doc L = global - doc_offset (docs <= L of that score pass),
 // clamped to n_docs; L < 0 (the tie doc lies in an earlier shard) becomes
 // "strictly higher scores only" = (score key + 1, any doc).
-__global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restrict__ all_keys,
+// The threshold by radix selection, one wave per query (no barriers; the
+// sort-based form (topk_of) took 43 us per search, a fixed cost that is
+// 7 % of an 8-way shard's batch): the k-th largest of the query's W * S
+// sample keys, decided bit by bit from the top — the answer has a bit set iff
+// at least `need` keys match its prefix with that bit set (need = k minus the
+// keys already ranked above).  Keys in registers when the query has at most
+// 1024 of them, re-read (L1) otherwise.
+constexpr int kThetaR = 16;  // keys per lane held in registers
+
+__global__ __launch_bounds__(256) void theta_wave_kernel(const uint64_t* __restrict__ all_keys,
                                                          int64_t W, int64_t Q, int64_t S,
                                                          int32_t k, uint64_t* __restrict__ theta,
                                                          int32_t* __restrict__ list_cnt,
                                                          int32_t C, int32_t nonneg,
                                                          int64_t doc_offset, int64_t n_docs) {
-  __shared__ uint64_t keys[kMergeP];
-  const int64_t q = blockIdx.x;
-  topk_of(SrcShards{all_keys, Q, S, q}, W * S, k, keys);
-  if (threadIdx.x == 0) {
-    uint64_t t = keys[k - 1];
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= Q) return;  // wave-uniform; no barriers
+  const uint32_t lane = lane_id();
+  const int64_t n = W * S;
+  uint64_t t = 0ull;
+  if (k > 0 && n >= k) {
+    uint64_t prefix = 0ull;
+    uint32_t need = (uint32_t)k;
+    if (n <= 64 * kThetaR) {
+      uint64_t key[kThetaR];
+#pragma unroll
+      for (int j = 0; j < kThetaR; ++j) {
+        const int64_t i = (int64_t)j * 64 + lane;
+        const int64_t w = i / S;
+        key[j] = i < n ? all_keys[(w * Q + q) * S + (i - w * S)] : 0ull;
+      }
+      for (int bit = 63; bit >= 0; --bit) {
+        const uint64_t hm = ~0ull << bit, cand = prefix | (1ull << bit);
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < kThetaR; ++j) c += (key[j] & hm) == cand;
+        const uint32_t tot = wave_sum_u32(c);
+        if (tot >= need) prefix = cand;
+        else need -= tot;
+      }
+    } else {
+      for (int bit = 63; bit >= 0; --bit) {
+        const uint64_t hm = ~0ull << bit, cand = prefix | (1ull << bit);
+        uint32_t c = 0;
+        for (int64_t w = 0; w < W; ++w) {
+          const uint64_t* kk = all_keys + (w * Q + q) * S;
+          for (int64_t i = lane; i < S; i += 64) c += (kk[i] & hm) == cand;
+        }
+        const uint32_t tot = wave_sum_u32(c);
+        if (tot >= need) prefix = cand;
+        else need -= tot;
+      }
+    }
+    t = prefix;
+  }
+  if (lane == 0) {
     if (t != 0ull) {
       const int64_t L = (int64_t)(0xFFFFFFFFu - (uint32_t)t) - doc_offset;
       if (L < 0)
@@ -2483,6 +2532,7 @@ __global__ __launch_bounds__(kMergeNT) void theta_kernel(const uint64_t* __restr
     if (t == 0ull && !nonneg) list_cnt[q] = C + 1;
   }
 }
+
 
 __device__ __forceinline__ int64_t stage_nq(const Stage& sg) {
   return sg.nq_dev ? (int64_t)*sg.nq_dev : (int64_t)sg.nq_host;
@@ -2723,7 +2773,8 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
     }
   }
   const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH, QMAP, DIAG, SM>);
-  hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrInts, st);
+  int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;
+  if (!sg.ctr_zeroed) hipMemsetAsync(wctr, 0, sizeof(int32_t) * kWctrInts, st);
   uint64_t* stamps = nullptr;
   if (DIAG & 32) {
     static uint64_t* buf = nullptr;
@@ -2734,7 +2785,7 @@ static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const S
   hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG, SM>), dim3((unsigned)grid),
                      dim3(64 * kWaves), 0, st, args_of(ix), q, (int32_t)T, sg.P, sg.nq_host,
                      sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, ws.list, ws.list_cnt, ws.list_cap,
-                     ws.wctr, claim_ch(), claim_m(), sg.cstride, sg.G, band_tiles(), stamps);
+                     wctr, claim_ch(), claim_m(), sg.cstride, sg.G, band_tiles(), stamps);
   if ((DIAG & 32) && PH == kRest) {
     std::vector<uint64_t> h(8 * grid * kWaves);
     hipStreamSynchronize(st);
@@ -2795,7 +2846,8 @@ static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const S
       return;
     }
   }
-  hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrInts, st);
+  int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;
+  if (!sg.ctr_zeroed) hipMemsetAsync(wctr, 0, sizeof(int32_t) * kWctrInts, st);
   // REST skips the sample tiles whose best key is below theta (m = 1 samples
   // in groups of one band: ws.cand holds this shard's sample keys)
   const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kBandW;
@@ -2808,7 +2860,7 @@ static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const S
     const int64_t nt = PH == kSample ? sample_count(ix.ntiles, sg.P, sg.G) : ix.ntiles;          \
     hipLaunchKernelGGL((score_flat_kernel<S, PH, SM, SPV>), dim3((unsigned)grid), dim3(64), 0, st, \
                        a, q, (int32_t)T, sg.P, sg.G, sg.nq_host, ws.theta, sg.cand_out,           \
-                       sg.cstride, ws.list, ws.list_cnt, ws.list_cap, ws.wctr, band_claim(),      \
+                       sg.cstride, ws.list, ws.list_cnt, ws.list_cap, wctr, band_claim(),         \
                        claim_m(), skip ? sg.sample_keys : nullptr, sg.sample_stride,              \
                        flat_band(nt, sg.nq_host, grid));                                          \
   }
@@ -2824,14 +2876,14 @@ static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const S
     hipLaunchKernelGGL((score_band_kernel<S, PH, SM, true>), dim3((unsigned)grid),
                        dim3(64 * kBandWaves), 0, st, a, q, (int32_t)T, sg.P, sg.G, sg.nq_host,
                        ws.theta, sg.cand_out, sg.cstride, ws.list, ws.list_cnt, ws.list_cap,
-                       ws.wctr, band_claim(), claim_m(), skip ? sg.sample_keys : nullptr,
+                       wctr, band_claim(), claim_m(), skip ? sg.sample_keys : nullptr,
                        sg.sample_stride);
     return;
   }
   const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM, false>, 64 * kBandWaves);
   hipLaunchKernelGGL((score_band_kernel<S, PH, SM, false>), dim3((unsigned)grid),
                      dim3(64 * kBandWaves), 0, st, a, q, (int32_t)T, sg.P, sg.G, sg.nq_host, ws.theta,
-                     sg.cand_out, sg.cstride, ws.list, ws.list_cnt, ws.list_cap, ws.wctr,
+                     sg.cand_out, sg.cstride, ws.list, ws.list_cnt, ws.list_cap, wctr,
                      band_claim(), claim_m(), skip ? sg.sample_keys : nullptr, sg.sample_stride);
 }
 
@@ -2968,14 +3020,31 @@ static Stage fallback_stage(const DevIndex& ix, int64_t Q, const Workspace& ws) 
   return sg;
 }
 
+__global__ __launch_bounds__(256) void zero_search_kernel(uint64_t* __restrict__ keys, int64_t nk,
+                                                          int32_t* __restrict__ wctr, int64_t nw,
+                                                          int32_t* __restrict__ counters,
+                                                          int32_t* __restrict__ list_cnt, int64_t Q) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, st = (int64_t)gridDim.x * 256;
+  for (int64_t i = i0; i < nk; i += st) keys[i] = 0ull;
+  for (int64_t i = i0; i < nw; i += st) wctr[i] = 0;
+  for (int64_t i = i0; i < Q; i += st) list_cnt[i] = 0;
+  if (i0 < 4) counters[i0] = 0;
+}
+
 // SAMPLE pass: each query's S keys into keys[Q][S] (zero-padded); a copy
 // stays in ws.cand for the REST pass's sample-tile skip.
 template <int S_>
 static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
                      const SampleGeom& g, uint64_t* keys, const Workspace& ws, hipStream_t st) {
-  hipMemsetAsync(keys, 0, sizeof(uint64_t) * Q * g.S, st);
+  // one launch zeroes everything the search counts into: the sample keys, the
+  // claim counters of SAMPLE, REST and the fallback, the rescore/fallback
+  // counters and the list counts (each was a memset launch: ~5 us apiece)
+  hipLaunchKernelGGL(zero_search_kernel, dim3(64), dim3(256), 0, st, keys, Q * g.S, ws.wctr,
+                     (int64_t)kWctrRegions * kWctrInts, ws.counters, ws.list_cnt, Q);
   if (ix.sparse && use_band(ix, T)) launch_seg_table(ix, q, Q, T, ws, st);  // SAMPLE + REST
   Stage sg = main_stage(ix, Q, g.P, ws);
+  sg.ctr_region = 0;
+  sg.ctr_zeroed = true;
   sg.M = g.m;
   sg.G = g.G;
   sg.cand_out = keys;
@@ -2991,18 +3060,21 @@ template <int S_>
 static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
                      const SampleGeom& g, int W, const uint64_t* all_keys, const Workspace& ws,
                      hipStream_t st) {
-  hipMemsetAsync(ws.counters, 0, 4 * sizeof(int32_t), st);
   Stage sg = main_stage(ix, Q, g.P, ws);
-  if (g.P == 1) {
+  if (g.P == 1) {  // no sample pass ran: nothing was zeroed
+    hipMemsetAsync(ws.counters, 0, 4 * sizeof(int32_t), st);
+    sg.ctr_region = 2;
+    sg.ctr_zeroed = false;
     launch_wave<S_, kAll>(ix, q, T, sg, ws, st);
     return;
   }
-  hipMemsetAsync(ws.list_cnt, 0, sizeof(int32_t) * Q, st);
+  sg.ctr_region = 1;  // counters, list counts and claim counters: zeroed by sample_s
+  sg.ctr_zeroed = true;
   sg.M = g.m;
   sg.G = g.G;
   sg.sample_keys = ws.cand;  // launch_sample left this shard's keys there
   sg.sample_stride = g.S;
-  hipLaunchKernelGGL(theta_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, st, all_keys,
+  hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, st, all_keys,
                      (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap,
                      ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs);
   launch_wave<S_, kRest>(ix, q, T, sg, ws, st);
@@ -3074,7 +3146,9 @@ static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   // queries whose list overflowed: exact pass over every tile (usually none;
   // the kernels read their count on the device and exit at once)
   hipMemsetAsync(ws.counters, 0, 2 * sizeof(int32_t), st);
-  const Stage fb = fallback_stage(ix, Q, ws);
+  Stage fb = fallback_stage(ix, Q, ws);
+  fb.ctr_region = 2;  // unused by the sampled search: zeroed by sample_s
+  fb.ctr_zeroed = true;
   launch_wave<S_, kAll>(ix, q, T, fb, ws, st);
   select_stage<S_>(ix, q, T, k, fb, ws, docs, scores, st);
 }
