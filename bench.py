@@ -143,7 +143,7 @@ def main():
     import torch
     from bm25mi import synth
     from bm25mi.index import GpuIndex
-    from bm25mi.dist import gpu_merge, sharded_search
+    from bm25mi.dist import sharded_search
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -190,13 +190,12 @@ def main():
     d_docs = torch.empty((Q, k), dtype=torch.int32, device=dev)
     d_scores = torch.empty((Q, k), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
-    merge = gpu_merge(local, stream)
 
     sdm = max(b - a for a, b in (synth.shard_bounds(cfg.n_docs, world, r) for r in range(world)))
 
     def step():
         if world > 1:  # global theta: RCCL all-gathers of sample keys and [Q, k] lists (bm25mi.dist)
-            sharded_search(index, dq, k, sdm, d_docs, d_scores, merge, stream)
+            sharded_search(index, dq, k, sdm, d_docs, d_scores, None, stream)
         else:
             index.search_device(dq, k, d_docs, d_scores, stream)
 

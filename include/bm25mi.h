@@ -176,6 +176,20 @@ int bm25_merge_topk_device(int device, const int32_t* d_docs,
                            void* stream);
 
 /*
+ * The same merge for lists that are each already best first — what
+ * bm25_search_finish_device writes (padding, doc -1 / key 0, last) — in one
+ * buffer per rank: rank w's [Q, k] docs and scores start at element
+ * w * rank_stride of d_docs / d_scores (rank_stride = Q * k for plain
+ * [W, Q, k] arrays, 2 * Q * k for the packed [W][docs|scores][Q][k] buffer
+ * one all-gather moves).  A W-way merge, one wavefront per query.
+ * Replaces: the reference is single-device (main.py:205); SURVEY.md §8(e).
+ */
+int bm25_merge_sorted_device(int device, const int32_t* d_docs,
+                             const float* d_scores, int64_t W, int64_t Q,
+                             int32_t k, int64_t rank_stride, int32_t* d_out_docs,
+                             float* d_out_scores, void* stream);
+
+/*
  * Doc-sharded search with a GLOBAL threshold, one rank per GPU (the
  * multi-process form of bm25_search_device).  Every rank
  * holds one doc shard (bm25_index_create with its doc_offset) and searches

@@ -58,6 +58,8 @@ _SIGS = {
     "bm25_scores_dense": ([_P, _P, _I64, _P], ctypes.c_int),
     "bm25_merge_topk_device": ([ctypes.c_int, _P, _P, _I64, _I64, _I32, _P, _P, _P],
                                ctypes.c_int),
+    "bm25_merge_sorted_device": ([ctypes.c_int, _P, _P, _I64, _I64, _I32, _I64, _P, _P, _P],
+                                 ctypes.c_int),
     "bm25_profile_enable": ([_P, ctypes.c_int], ctypes.c_int),
     "bm25_profile_read": ([_P, _PD, _PI64, _PD, _PI64, _PI64], ctypes.c_int),
     "bm25_search_stats": ([_P, _PI64, _PI64], ctypes.c_int),

@@ -94,7 +94,8 @@ def gather_keys(keys: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -
 
 
 def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
-                   d_docs: torch.Tensor, d_scores: torch.Tensor, merge: MergeFn, stream=None,
+                   d_docs: torch.Tensor, d_scores: torch.Tensor,
+                   merge: Optional[MergeFn] = None, stream=None,
                    group: Optional[dist.ProcessGroup] = None,
                    exchange: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
                    ) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -103,7 +104,10 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
     the k-th best key of the whole sample, the shard lists its keys >= theta,
     and the lists are all-gathered and merged.  Two collectives per batch:
     W*Q*S*8 B of sample keys (S ~ 2k/W: ~200 KB per rank at config 3) and the
-    [Q, k] lists.  ``exchange`` replaces the key all-gather (tests).
+    [Q, k] lists — docs and scores in one packed [2, Q, k] buffer, merged by
+    the W-way merge of best-first lists (bm25_merge_sorted_device) unless a
+    ``merge`` of the two gathered arrays is given.  ``exchange`` replaces the
+    key all-gather (tests).
 
     Everything — kernels and collectives — is enqueued on ``stream`` (default:
     the current stream): the collectives order against torch's current
@@ -125,8 +129,18 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
             all_keys = gather_keys(keys, group)
         else:
             all_keys = keys.unsqueeze(0)
-        index.search_finish_device(d_queries, k, world, shard_docs_max, all_keys, d_docs,
-                                   d_scores, stream)
-        if exchange is not None:
-            return d_docs, d_scores
-        return sharded_topk(d_docs, d_scores, merge, group)
+        packed = merge is None and exchange is None and world > 1
+        if not packed:
+            index.search_finish_device(d_queries, k, world, shard_docs_max, all_keys, d_docs,
+                                       d_scores, stream)
+            if exchange is not None or world == 1:
+                return d_docs, d_scores
+            return sharded_topk(d_docs, d_scores, merge, group)
+        pk = torch.empty((2, Q, k), dtype=torch.int32, device=d_queries.device)
+        index.search_finish_device(d_queries, k, world, shard_docs_max, all_keys, pk[0],
+                                   pk[1].view(torch.float32), stream)
+        g = _all_gather(pk, group)  # [W, 2, Q, k]: one collective for docs and scores
+        from .index import merge_sorted_device
+        merge_sorted_device(d_queries.device.index, g, g[:, 1].view(torch.float32), world, Q, k,
+                            2 * Q * k, d_docs, d_scores, stream)
+        return d_docs, d_scores

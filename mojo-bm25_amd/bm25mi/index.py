@@ -205,6 +205,19 @@ def merge_topk_device(device: int, d_docs, d_scores, W: int, Q: int, k: int, d_o
                                      ctypes.c_void_p(s)))
 
 
+def merge_sorted_device(device: int, d_docs, d_scores, W: int, Q: int, k: int, rank_stride: int,
+                        d_out_docs, d_out_scores, stream=None) -> None:
+    """W-way merge of best-first [Q, k] lists (bm25_merge_sorted_device):
+    rank w's lists start at element w * rank_stride of d_docs / d_scores."""
+    s = getattr(stream, "cuda_stream", stream) or 0
+    check(lib.bm25_merge_sorted_device(int(device), ctypes.c_void_p(d_docs.data_ptr()),
+                                       ctypes.c_void_p(d_scores.data_ptr()), int(W), int(Q),
+                                       int(k), int(rank_stride),
+                                       ctypes.c_void_p(d_out_docs.data_ptr()),
+                                       ctypes.c_void_p(d_out_scores.data_ptr()),
+                                       ctypes.c_void_p(s)))
+
+
 class ShardedIndex:
     """A CSC index doc-sharded over several GPUs of this process
     (bm25_sharded_* in include/bm25mi.h): ``search`` has GpuIndex.search's

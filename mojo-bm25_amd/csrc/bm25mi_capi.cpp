@@ -694,7 +694,21 @@ int bm25_merge_topk_device(int device, const int32_t* d_docs, const float* d_sco
   if (W < 1 || Q < 0 || k < 0) return fail(BM25_EINVAL, "bad merge shape W=%lld Q=%lld k=%d", (long long)W, (long long)Q, k);
   if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%d exceeds the engine limit %d", k, kMaxK);
   HIP_TRY(hipSetDevice(device), "hipSetDevice");
-  HIP_TRY(launch_merge_lists(d_docs, d_scores, W, Q, k, d_out_docs, d_out_scores, (hipStream_t)stream), "merge_lists launch");
+  HIP_TRY(launch_merge_lists(d_docs, d_scores, W, Q, k, Q * (int64_t)k, false, d_out_docs, d_out_scores, (hipStream_t)stream), "merge_lists launch");
+  return BM25_OK;
+}
+
+int bm25_merge_sorted_device(int device, const int32_t* d_docs, const float* d_scores, int64_t W,
+                             int64_t Q, int32_t k, int64_t rank_stride, int32_t* d_out_docs,
+                             float* d_out_scores, void* stream) {
+  if (W < 1 || Q < 0 || k < 0 || rank_stride < Q * (int64_t)k)
+    return fail(BM25_EINVAL, "bad merge shape W=%lld Q=%lld k=%d stride=%lld", (long long)W,
+                (long long)Q, k, (long long)rank_stride);
+  if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%d exceeds the engine limit %d", k, kMaxK);
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+  HIP_TRY(launch_merge_lists(d_docs, d_scores, W, Q, k, rank_stride, true, d_out_docs,
+                             d_out_scores, (hipStream_t)stream),
+          "merge_sorted launch");
   return BM25_OK;
 }
 
@@ -996,7 +1010,7 @@ int bm25_sharded_search(bm25_sharded* s, const int32_t* queries, int64_t Q, int6
     HIP_TRY(hipMemcpyPeerAsync(s->g_scores + r * out, h0->ix.device, h->d_scores, h->ix.device,
                                sizeof(float) * out, h0->stream), "peer copy");
   }
-  HIP_TRY(launch_merge_lists(s->g_docs, s->g_scores, W, Q, k, s->m_docs, s->m_scores, h0->stream),
+  HIP_TRY(launch_merge_lists(s->g_docs, s->g_scores, W, Q, k, Q * (int64_t)k, true, s->m_docs, s->m_scores, h0->stream),
           "merge_lists launch");
   HIP_TRY(hipMemcpyAsync(out_docs, s->m_docs, sizeof(int32_t) * out, hipMemcpyDeviceToHost,
                          h0->stream), "D2H docs");

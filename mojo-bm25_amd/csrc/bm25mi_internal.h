@@ -154,9 +154,11 @@ hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries,
                          int32_t* d_docs, float* d_scores, hipStream_t stream);
 hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query,
                                int64_t T, float* d_out, hipStream_t stream);
+// W lists [Q, k] at element w * rank_stride (docs and scores alike) -> [Q, k];
+// sorted: every list is already best-first (W-way merge instead of a sort).
 hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores,
-                              int64_t W, int64_t Q, int k, int32_t* d_out_docs,
-                              float* d_out_scores, hipStream_t stream);
+                              int64_t W, int64_t Q, int k, int64_t rank_stride, bool sorted,
+                              int32_t* d_out_docs, float* d_out_scores, hipStream_t stream);
 
 // Largest token id of [n] device ids (0 if none is positive) into *d_out.
 hipError_t launch_max_token(const int32_t* d_queries, int64_t n, int32_t* d_out,

@@ -2433,14 +2433,15 @@ struct SrcFinal {
   }
 };
 
-struct SrcLists {
+struct SrcLists {  // list w of query q at element w * rstride + q * k
   const int32_t* docs;
   const float* scores;
   int64_t Q, q;
   int k;
+  int64_t rstride;
   __device__ uint64_t operator()(int64_t i) const {
     const int64_t w = i / k, j = i - w * k;
-    const int64_t o = (w * Q + q) * k + j;
+    const int64_t o = w * rstride + q * k + j;
     return make_key(scores[o], (uint32_t)docs[o]);
   }
 };
@@ -2638,11 +2639,57 @@ __global__ __launch_bounds__(kMergeNT) void merge_final_kernel(
 
 __global__ __launch_bounds__(kMergeNT) void merge_lists_kernel(
     const int32_t* __restrict__ in_docs, const float* __restrict__ in_scores, int64_t W,
-    int64_t Q, int32_t k, int32_t* __restrict__ docs, float* __restrict__ scores) {
+    int64_t Q, int32_t k, int64_t rstride, int32_t* __restrict__ docs, float* __restrict__ scores) {
   __shared__ uint64_t keys[kMergeP];
   const int64_t q = blockIdx.x;
-  topk_of(SrcLists{in_docs, in_scores, Q, q, k}, W * k, k, keys);
+  topk_of(SrcLists{in_docs, in_scores, Q, q, k, rstride}, W * k, k, keys);
   write_result(keys, k, q, 0, docs, scores);
+}
+
+// Merge of W lists that are each sorted best first (bm25_search_finish_
+// device's [Q, k] lists, padding last): one wave per query, the W list heads
+// in lanes 0..W-1; each of the k steps takes the best head (wave max of the
+// u64 key, as two u32 maxima) and advances that list.  A query's lists are
+// staged in LDS first (W * k <= kMergeSortedCap keys); larger merges take
+// merge_lists_kernel.  Keys are unique (global doc ids) except padding (0).
+constexpr int kMergeSortedCap = 1024;  // keys per wave
+
+__global__ __launch_bounds__(256) void merge_sorted_kernel(
+    const int32_t* __restrict__ in_docs, const float* __restrict__ in_scores, int32_t W,
+    int64_t Q, int32_t k, int64_t rstride, int32_t* __restrict__ docs,
+    float* __restrict__ scores) {
+  __shared__ uint64_t buf[4][kMergeSortedCap];
+  const int wave = (int)(threadIdx.x >> 6);
+  const int64_t q = (int64_t)blockIdx.x * 4 + wave;
+  if (q >= Q) return;  // wave-uniform; no barriers
+  uint64_t* kb = buf[wave];
+  const uint32_t lane = lane_id();
+  const int n = W * k;
+  for (int i = (int)lane; i < n; i += 64) {
+    const int w = i / k, j = i - w * k;
+    const int64_t o = (int64_t)w * rstride + q * k + j;
+    kb[i] = make_key(in_scores[o], (uint32_t)in_docs[o]);
+  }
+  int pos = 0;
+  uint64_t head = ((int)lane < W) ? kb[lane * k] : 0ull;
+  for (int j = 0; j < k; ++j) {
+    const uint32_t hh = wave_max_u32((uint32_t)(head >> 32));
+    const uint32_t hl = wave_max_u32((uint32_t)(head >> 32) == hh ? (uint32_t)head : 0u);
+    const uint64_t best = ((uint64_t)hh << 32) | hl;
+    if (lane == 0) {
+      if (best == 0ull) {  // every list is down to its padding
+        docs[q * k + j] = -1;
+        scores[q * k + j] = __uint_as_float(0xFFFFFFFFu);
+      } else {
+        docs[q * k + j] = (int32_t)(0xFFFFFFFFu - (uint32_t)best);
+        scores[q * k + j] = key_score(hh);
+      }
+    }
+    if (best != 0ull && head == best) {
+      ++pos;
+      head = pos < k ? kb[lane * k + pos] : 0ull;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2821,13 +2868,13 @@ static bool use_flat() {
 }
 
 // Tiles per flat-kernel item: 8, halved while the phase would give the
-// resident waves fewer than BM25_ITEMS_PER_WAVE (24) items each — a small doc
+// resident waves fewer than BM25_ITEMS_PER_WAVE (8) items each — a small doc
 // shard's SAMPLE pass has ~2 eight-tile items per wave, and the last wave's
 // items set the pass time (BM25_FLAT_BW forces a width).
 static int32_t flat_band(int64_t nt, int64_t nq, int grid) {
   static const int forced = getenv("BM25_FLAT_BW") ? atoi(getenv("BM25_FLAT_BW")) : 0;
   if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
-  static const int64_t per = getenv("BM25_ITEMS_PER_WAVE") ? atoi(getenv("BM25_ITEMS_PER_WAVE")) : 24;
+  static const int64_t per = getenv("BM25_ITEMS_PER_WAVE") ? atoi(getenv("BM25_ITEMS_PER_WAVE")) : 8;
   int32_t bw = 8;
   while (bw > 1 && ((nt + bw - 1) / bw) * nq < per * (int64_t)grid) bw >>= 1;
   return bw;
@@ -3184,11 +3231,17 @@ hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query, int64
 }
 
 hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores, int64_t W,
-                              int64_t Q, int k, int32_t* d_out_docs, float* d_out_scores,
-                              hipStream_t stream) {
+                              int64_t Q, int k, int64_t rank_stride, bool sorted,
+                              int32_t* d_out_docs, float* d_out_scores, hipStream_t stream) {
   if (Q == 0 || k == 0) return hipSuccess;
+  if (sorted && W * k <= kMergeSortedCap && W <= 64) {
+    hipLaunchKernelGGL(merge_sorted_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, stream,
+                       d_docs, d_scores, (int32_t)W, Q, (int32_t)k, rank_stride, d_out_docs,
+                       d_out_scores);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(merge_lists_kernel, dim3((unsigned)Q), dim3(kMergeNT), 0, stream, d_docs,
-                     d_scores, W, Q, (int32_t)k, d_out_docs, d_out_scores);
+                     d_scores, W, Q, (int32_t)k, rank_stride, d_out_docs, d_out_scores);
   return hipGetLastError();
 }
 

@@ -270,6 +270,46 @@ def test_sharded_merge_equals_single_index(gpu):
     _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)
 
 
+@pytest.mark.parametrize("W,k", [(2, 1), (3, 100), (8, 100), (8, 128), (5, 300)])
+def test_merge_sorted_packed_lists(gpu, W, k):
+    """bm25_merge_sorted_device on the packed [W][docs|scores][Q][k] buffer of
+    the doc-sharded path: best-first lists (global doc ids, some padded with
+    doc -1 / key 0, tied scores across ranks) merge to the (score desc, doc
+    asc) top-k — the same bits as the sort-based bm25_merge_topk_device, and
+    as a numpy merge.  W * k > 1024 takes the sort kernel with the stride."""
+    import torch
+    from bm25mi.index import merge_sorted_device, merge_topk_device
+    rng = np.random.default_rng(W * 1000 + k)
+    Q = 37
+    docs = np.full((W, Q, k), -1, np.int32)
+    scores = np.full((W, Q, k), np.uint32(0xFFFFFFFF).view(np.float32), np.float32)
+    for w in range(W):
+        for q in range(Q):
+            n = int(rng.integers(0, k + 1)) if q % 5 else k
+            d = rng.choice(np.arange(w, 200_000, W), size=n, replace=False).astype(np.int32)
+            s = np.round(rng.uniform(0, 4, size=n) * 8).astype(np.float32) / 8  # ties
+            o = np.lexsort((d, -s))
+            docs[w, q, :n], scores[w, q, :n] = d[o], s[o]
+    pk = np.stack([docs, scores.view(np.int32)], axis=1)  # [W, 2, Q, k]
+    g = torch.from_numpy(np.ascontiguousarray(pk)).cuda()
+    md = torch.empty((Q, k), dtype=torch.int32, device="cuda")
+    ms = torch.empty((Q, k), dtype=torch.float32, device="cuda")
+    merge_sorted_device(0, g, g[:, 1].view(torch.float32), W, Q, k, 2 * Q * k, md, ms)
+    rd = torch.empty_like(md)
+    rs = torch.empty_like(ms)
+    merge_topk_device(0, torch.from_numpy(docs).cuda(), torch.from_numpy(scores).cuda(), W, Q, k,
+                      rd, rs)
+    torch.cuda.synchronize()
+    _exact((md.cpu().numpy(), ms.cpu().numpy()), (rd.cpu().numpy(), rs.cpu().numpy()))
+    for q in range(Q):
+        d, s = docs[:, q].ravel(), scores[:, q].ravel()
+        real = d >= 0
+        o = np.lexsort((d[real], -s[real]))[:k]
+        n = len(o)
+        assert np.array_equal(md[q, :n].cpu().numpy(), d[real][o])
+        assert (md[q, n:].cpu().numpy() == -1).all()
+
+
 def test_config2_full_parity(gpu):
     from bm25mi import synth
     cfg = synth.CONFIGS["c2"]
