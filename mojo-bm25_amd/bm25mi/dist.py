@@ -120,7 +120,9 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
         if exchange is not None:
             world = int(exchange.world)  # type: ignore[attr-defined]
         S = index.sample_width(k, world, shard_docs_max)
-        keys = torch.zeros((Q, max(S, 1)), dtype=torch.int64, device=d_queries.device)
+        # S > 0: the sample pass zeroes the keys itself (zero_search_kernel)
+        keys = (torch.empty if S > 0 else torch.zeros)((Q, max(S, 1)), dtype=torch.int64,
+                                                       device=d_queries.device)
         if S > 0:
             index.search_sample_device(d_queries, k, world, shard_docs_max, keys, stream)
         if exchange is not None:
