@@ -525,7 +525,8 @@ __device__ __forceinline__ int64_t tile_of(int64_t ti, int P, int G) {
 }
 template <int PH>
 __device__ __forceinline__ int32_t tile_of32(uint32_t ti, uint32_t P, uint32_t G) {
-  return (int32_t)(PH == kSample ? (ti / G) * G * P + ti % G : ti);
+  // G (1 or kSampleGroup) is a power of two: no integer division
+  return (int32_t)(PH == kSample ? ((ti & ~(G - 1u)) * P) | (ti & (G - 1u)) : ti);
 }
 
 
@@ -2132,8 +2133,9 @@ constexpr int kRescoreNT = 256;
 __device__ __forceinline__ void bitonic_sort_desc(uint64_t* keys, int n) {
   for (int size = 2; size <= n; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < (n >> 1); i += blockDim.x) {
-        const int lo = 2 * stride * (i / stride) + (i % stride);
+      const int ls = __builtin_ctz((unsigned)stride);  // stride is a power of two:
+      for (int i = threadIdx.x; i < (n >> 1); i += blockDim.x) {  // no integer division
+        const int lo = ((i >> ls) << (ls + 1)) + (i & (stride - 1));
         const int hi = lo + stride;
         const bool desc = (lo & size) == 0;
         const uint64_t x = keys[lo], y = keys[hi];
