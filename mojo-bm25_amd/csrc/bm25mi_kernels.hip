@@ -1784,7 +1784,7 @@ __global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu
 #define BM25_FR 10
 #endif
 #ifndef BM25_FR_S
-#define BM25_FR_S 10
+#define BM25_FR_S 8
 #endif
 constexpr uint32_t kDeadSid = 0xFFFFFFFFu;   // padding row: no adds, no tile
 constexpr uint32_t kNoTag = 0xFFFFFFFFu;     // accumulator holds no tile
@@ -1908,6 +1908,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // REST: sample tiles (groups of G = kSampleGroup tiles, one group per G * P)
   // whose best sample key is below theta are skipped
   const bool skipping = PH == kRest && skeys != nullptr && G == kSampleGroup;
+  const uint32_t lgG = (uint32_t)__builtin_ctz((unsigned)G), lgP = (uint32_t)__builtin_ctz((unsigned)P);
   auto load_bdesc = [&](const BandCur& c, int32_t tm) -> BandDesc {
     BandDesc d;
     const int32_t term = __shfl(tm, (int)lt, 64);
@@ -1929,8 +1930,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       d.r1 = r[1];
     }
     d.ok = ok ? 1u : 0u;
-    const bool smp = skipping && ok && ((tile / G) % P) == 0;
-    const int64_t si = (tile / ((int64_t)G * P)) * G + tile % G;
+    // G and P are powers of two (sample_geom): shifts, no integer division
+    const uint32_t t32 = (uint32_t)tile;
+    const bool smp = skipping && ok && ((t32 >> lgG) & (uint32_t)(P - 1)) == 0u;
+    const int64_t si = (int64_t)(((t32 >> (lgG + lgP)) << lgG) | (t32 & (uint32_t)(G - 1)));
     d.skey = smp ? skeys[(int64_t)c.q * sstride + min<int64_t>(si, sstride - 1)] : ~0ull;
     return d;
   };
