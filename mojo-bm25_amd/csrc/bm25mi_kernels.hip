@@ -1804,6 +1804,11 @@ __device__ __forceinline__ uint32_t scan64(uint32_t x) {
   return x;
 }
 
+struct FlatDesc {   // lane i * 8 + t: term t's segment in tile i (raw; r1 == r0: none)
+  uint32_t ip, r0, r1;
+  uint32_t sk;      // REST: score-key half of the tile's best sample key (sample tiles)
+};
+
 struct FlatTab {    // one chunk of an item's rows: lane r = row j0 + r
   uint32_t base;    // even posting index of the row's first pair (0: dead row)
   uint32_t pk;      // valid postings [lo, hi) of the row's 128 (lo = pk & 1, hi = pk >> 1)
@@ -1909,8 +1914,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // whose best sample key is below theta are skipped
   const bool skipping = PH == kRest && skeys != nullptr && G == kSampleGroup;
   const uint32_t lgG = (uint32_t)__builtin_ctz((unsigned)G), lgP = (uint32_t)__builtin_ctz((unsigned)P);
-  auto load_bdesc = [&](const BandCur& c, int32_t tm) -> BandDesc {
-    BandDesc d;
+  // an item's segment descriptors (4 VGPRs: a lane outside the item reads its
+  // r1 from r0's address, so r1 - r0 = 0 needs no flag; the sample-tile test
+  // is redone from the item cursor at enter_item)
+  auto load_bdesc = [&](const BandCur& c, int32_t tm) -> FlatDesc {
+    FlatDesc d;
     const int32_t term = __shfl(tm, (int)lt, 64);
     const bool ok = (int)lt < T && (int)li < c.bw && term >= 0 && term < a.V;
     const int64_t tt = ok ? term : 0;
@@ -1927,14 +1935,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       const uint32_t* r = a.rel + tt * (a.ntiles + 1) + tile;
       d.ip = (uint32_t)a.indptr[tt];
       d.r0 = r[0];
-      d.r1 = r[1];
+      d.r1 = *(ok ? r + 1 : r);
     }
-    d.ok = ok ? 1u : 0u;
-    // G and P are powers of two (sample_geom): shifts, no integer division
-    const uint32_t t32 = (uint32_t)tile;
-    const bool smp = skipping && ok && ((t32 >> lgG) & (uint32_t)(P - 1)) == 0u;
-    const int64_t si = (int64_t)(((t32 >> (lgG + lgP)) << lgG) | (t32 & (uint32_t)(G - 1)));
-    d.skey = smp ? skeys[(int64_t)c.q * sstride + min<int64_t>(si, sstride - 1)] : ~0ull;
+    if (skipping) {  // the score-key half of this tile's best sample key
+      // G and P are powers of two (sample_geom): shifts, no integer division
+      const uint32_t t32 = (uint32_t)tile;
+      const int64_t si = (int64_t)(((t32 >> (lgG + lgP)) << lgG) | (t32 & (uint32_t)(G - 1)));
+      d.sk = reinterpret_cast<const uint32_t*>(skeys)[2 * ((int64_t)c.q * sstride +
+                                                             min<int64_t>(si, sstride - 1)) + 1];
+    } else {
+      d.sk = 0u;
+    }
     return d;
   };
   auto th_positive = [&](uint64_t th) -> bool {
@@ -1947,15 +1958,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   uint32_t iTotal = 0, iR = 0, iJ0 = 0, iSer = 0;
   FlatCtx ctxI{0, 0, 0ull};
   BandCur nx, nx2;
-  BandDesc dN;
+  FlatDesc dN;
   uint64_t thN = 0ull;
   int32_t tmN2 = 0;
   // enter item nx (descriptors dN) on the issue side; advance the prefetch
   auto enter_item = [&]() {
     const bool th_pos = PH == kRest && th_positive(thN);
-    const bool skip = skipping && th_pos && (uint32_t)(dN.skey >> 32) < (uint32_t)(thN >> 32);
+    const uint32_t t32 = (uint32_t)(nx.b * BW) + li;  // REST: phase tile = tile
+    const bool smp = skipping && ((t32 >> lgG) & (uint32_t)(P - 1)) == 0u;
+    const bool skip = smp && th_pos && dN.sk < (uint32_t)(thN >> 32);
     iSb = dN.ip + dN.r0;
-    iSl = (dN.ok && !skip) ? dN.r1 - dN.r0 : 0u;
+    iSl = skip ? 0u : dN.r1 - dN.r0;
     uint32_t nr = iSl == 0u ? 0u : ((iSb & 1u) + iSl + 127u) >> 7;
     // no positive threshold: every tile of the band runs its epilogue (one
     // row, possibly empty, in each tile)
