@@ -1925,9 +1925,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b * BW + li), (uint32_t)P,
                                                       (uint32_t)G)
                             : 0;
-    if constexpr (SP) {
-      const uint64_t e =
-          ok ? a.seg[((int64_t)c.q * nbp + (tile >> 3)) * 64 + lt * 8 + (tile & 7)] : 0ull;
+    if constexpr (SP) {  // outside the item: the zero entry past the table
+      const uint64_t e = a.seg[ok ? ((int64_t)c.q * nbp + (tile >> 3)) * 64 + lt * 8 + (tile & 7)
+                                  : (int64_t)nq * nbp * 64];
       d.ip = 0u;
       d.r0 = (uint32_t)e;
       d.r1 = (uint32_t)e + (uint32_t)(e >> 32);
@@ -3004,8 +3004,8 @@ hipError_t launch_max_token(const int32_t* d_queries, int64_t n, int32_t* d_out,
   return hipGetLastError();
 }
 
-int64_t seg_entries(const DevIndex& ix, int64_t Q) {
-  return ix.sparse ? Q * ((ix.ntiles + 7) >> 3) * 64 : 0;
+int64_t seg_entries(const DevIndex& ix, int64_t Q) {  // + 64 zero entries past the table
+  return ix.sparse ? Q * ((ix.ntiles + 7) >> 3) * 64 + 64 : 0;
 }
 
 static void launch_seg_table(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
