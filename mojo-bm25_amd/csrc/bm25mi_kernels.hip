@@ -2515,15 +2515,40 @@ __global__ __launch_bounds__(256) void theta_wave_kernel(const uint64_t* __restr
         const int64_t w = i / S;
         key[j] = i < n ? all_keys[(w * Q + q) * S + (i - w * S)] : 0ull;
       }
-      for (int bit = 63; bit >= 0; --bit) {
-        const uint64_t hm = ~0ull << bit, cand = prefix | (1ull << bit);
+      // score half first (32 steps on u32), then the doc half among the keys
+      // of that score — only when more than one key holds it (ties)
+      uint32_t hi = 0u;
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t hm = ~0u << bit, cand = hi | (1u << bit);
         uint32_t c = 0;
 #pragma unroll
-        for (int j = 0; j < kThetaR; ++j) c += (key[j] & hm) == cand;
+        for (int j = 0; j < kThetaR; ++j) c += ((uint32_t)(key[j] >> 32) & hm) == cand;
         const uint32_t tot = wave_sum_u32(c);
-        if (tot >= need) prefix = cand;
+        if (tot >= need) hi = cand;
         else need -= tot;
       }
+      uint32_t ties = 0;
+#pragma unroll
+      for (int j = 0; j < kThetaR; ++j) ties += (uint32_t)(key[j] >> 32) == hi;
+      uint32_t lo = 0u;
+      if (wave_sum_u32(ties) == 1u) {  // the one key of that score
+        uint32_t m = 0u;
+#pragma unroll
+        for (int j = 0; j < kThetaR; ++j) m = (uint32_t)(key[j] >> 32) == hi ? (uint32_t)key[j] : m;
+        lo = wave_max_u32(m);
+      } else {
+        for (int bit = 31; bit >= 0; --bit) {
+          const uint32_t hm = ~0u << bit, cand = lo | (1u << bit);
+          uint32_t c = 0;
+#pragma unroll
+          for (int j = 0; j < kThetaR; ++j)
+            c += (uint32_t)(key[j] >> 32) == hi && ((uint32_t)key[j] & hm) == cand;
+          const uint32_t tot = wave_sum_u32(c);
+          if (tot >= need) lo = cand;
+          else need -= tot;
+        }
+      }
+      prefix = ((uint64_t)hi << 32) | lo;
     } else {
       for (int bit = 63; bit >= 0; --bit) {
         const uint64_t hm = ~0ull << bit, cand = prefix | (1ull << bit);
