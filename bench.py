@@ -65,55 +65,78 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def load_traffic(path: str, config: str, shift: int):
-    """HBM bytes per score_tiles launch measured offline with rocprofv3 --pmc
+def load_traffic(path: str, config: str, shift: int, terms: int):
+    """HBM bytes per score pass measured offline with rocprofv3 --pmc
     (profiles/) — used only if it matches this workload."""
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("config") == config and int(t.get("tile_shift", -1)) == shift:
+        if (t.get("config") == config and int(t.get("tile_shift", -1)) == shift
+                and int(t.get("terms_per_query", 8)) == terms):
             return t
     except (OSError, ValueError):
         pass
     return None
 
 
+def cpu_quota():
+    """CPUs this job may use: the cgroup v2 CPU quota (cpu.max) when one is
+    set, else the affinity mask."""
+    aff = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, min(aff, int(int(q) // int(period)))), aff, f"cgroup cpu.max {q} {period}"
+    except (OSError, ValueError):
+        pass
+    return aff, aff, "no cgroup quota"
+
+
 def cpu_baseline(args, n_docs, indptr, indices, data, queries, k):
     """BASELINE.md CPU legs on a seeded query sample: (i) one process, one
-    core; (ii) a fork-based process pool over the host cores this job may use.
-    The port is oracle.search_faithful — the reference's scipy/numpy call
-    sequence (bm25_native.py:147-158, 204-214)."""
+    core; (ii) a fork-based process pool over the cores this job may use
+    (BASELINE.md:54 names the affinity mask; the GPU box gives one GPU's job
+    a share of 16 CPUs — the pool is sized to that share, and the per-core
+    rate scaled to the whole affinity mask is reported beside it, labelled as
+    an extrapolation).  The port is oracle.search_faithful — the reference's
+    scipy/numpy call sequence (bm25_native.py:147-158, 204-214)."""
     from oracle import oracle  # the checker / CPU baseline (test infrastructure)
     Q = queries.shape[0]
-    nq = min(args.cpu_queries, Q)
+    quota, aff, why = cpu_quota()
+    share = int(os.environ.get("BM25_CPU_SHARE", "16"))
+    procs = args.cpu_procs if args.cpu_procs > 0 else min(quota, share)
+    nq1 = min(args.cpu_queries, Q)                 # single-core leg
+    nqp = min(Q, max(nq1, 4 * procs))              # pool leg: 4 queries per process
     rng = np.random.default_rng(20240601)
-    sample = queries[np.sort(rng.choice(Q, size=nq, replace=False))]
-    aff = len(os.sched_getaffinity(0))
-    procs = args.cpu_procs
-    if procs <= 0:
-        procs = aff
-        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
-            procs = min(procs, int(os.environ["OMP_NUM_THREADS"]))
-    procs = max(1, min(procs, nq))
+    order = rng.permutation(Q)
+    sample1 = queries[np.sort(order[:nq1])]
+    samplep = queries[np.sort(order[:nqp])]
     m = oracle.faithful_matrix(n_docs, indptr, indices, data)
-    log(f"[rank 0] CPU baseline: {nq} sampled queries, 1 process ...")
+    log(f"[rank 0] CPU baseline: {nq1} sampled queries, 1 process ...")
     t0 = time.perf_counter()
-    d1, s1 = oracle.search_faithful_m(m, sample, k)
+    d1, s1 = oracle.search_faithful_m(m, sample1, k)
     t1 = time.perf_counter() - t0
-    log(f"[rank 0] CPU baseline: {nq} sampled queries, pool of {procs} processes ...")
-    d2, s2, t2 = oracle.search_faithful_pool(m, sample, k, procs)
-    if not np.array_equal(s1.view(np.uint32), s2.view(np.uint32)):
+    log(f"[rank 0] CPU baseline: {nqp} sampled queries, pool of {procs} processes ...")
+    d2, s2, t2 = oracle.search_faithful_pool(m, samplep, k, procs)
+    pos = np.searchsorted(np.sort(order[:nqp]), np.sort(order[:nq1]))
+    if not np.array_equal(s1.view(np.uint32), s2[pos].view(np.uint32)):
         raise RuntimeError("CPU baseline legs disagree")
-    return {"value": round(nq / t2, 3), "unit": "queries/s", "cores": procs, "kind": "port",
-            "sample": f"{nq} queries drawn (seed 20240601) from the {Q}-query bench batch, same "
-                      f"index, k={k}; leg (ii): fork pool of {procs} processes, batch split "
-                      f"evenly; {t2:.2f} s; host {cpu_model()}, os.cpu_count()={os.cpu_count()}, "
-                      f"affinity {aff} cpus",
-            "single_core": {"value": round(nq / t1, 3), "unit": "queries/s", "cores": 1,
-                            "seconds": round(t1, 2)},
-            "batch_s_extrapolated": {"single_core": round(t1 / nq * Q, 1),
-                                     "pool": round(t2 / nq * Q, 1),
-                                     "note": f"EXTRAPOLATION: sample time x {Q}/{nq}"}}
+    per_core = nqp / t2 / procs
+    return {"value": round(nqp / t2, 3), "unit": "queries/s", "cores": procs, "kind": "port",
+            "sample": f"{nqp} queries drawn (seed 20240601) from the {Q}-query bench batch, same "
+                      f"index, k={k}; leg (ii): fork pool of {procs} processes (this job's CPU "
+                      f"share), batch split evenly; {t2:.2f} s; host {cpu_model()}, "
+                      f"os.cpu_count()={os.cpu_count()}, affinity {aff} cpus, {why}",
+            "single_core": {"value": round(nq1 / t1, 3), "unit": "queries/s", "cores": 1,
+                            "queries": nq1, "seconds": round(t1, 2)},
+            "affinity_extrapolation": {
+                "value": round(per_core * aff, 1), "unit": "queries/s", "cores": aff,
+                "note": f"EXTRAPOLATION: the pool's per-process rate ({per_core:.3f} q/s) x the "
+                        f"{aff} cpus of the affinity mask (BASELINE.md:54); not measured — the "
+                        f"job's CPU share is {procs}"},
+            "batch_s_extrapolated": {"single_core": round(t1 / nq1 * Q, 1),
+                                     "pool": round(t2 / nqp * Q, 1),
+                                     "note": f"EXTRAPOLATION: sample time x {Q}/sample"}}
 
 
 def main():
@@ -128,8 +151,11 @@ def main():
     ap.add_argument("--cpu-queries", type=int, default=64,
                     help="CPU baseline: seeded query sample size (0 = skip)")
     ap.add_argument("--cpu-procs", type=int, default=-1,
-                    help="CPU baseline pool leg: worker processes (default: the affinity "
-                         "mask's cores, capped at OMP_NUM_THREADS when that is set)")
+                    help="CPU baseline pool leg: worker processes (default: the job's CPU "
+                         "share, 16 on the GPU box, or the cgroup quota when smaller)")
+    ap.add_argument("--terms", type=int, default=0,
+                    help="terms per query (default: the config's, 8); e.g. 16 for the "
+                         "long-query workload line")
     ap.add_argument("--e2e-batches", type=int, default=20,
                     help="host-buffer searches (H2D queries -> D2H results) timed for the "
                          "end-to-end median")
@@ -151,6 +177,9 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     cfg = synth.CONFIGS[args.config]
+    if args.terms > 0:
+        import dataclasses
+        cfg = dataclasses.replace(cfg, terms_per_query=args.terms)
     # config 5 holds 6.4B postings: one GPU runs one of the 8 ranks' shards
     # (800M postings, int64 global indptr cut per rank by the generator)
     emul = 8 if (args.config == "c5" and world == 1) else 0
@@ -219,6 +248,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     prof = index.profile_read()
+    dispatch = index.last_dispatch()
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     # end-to-end (N=1): the host-buffer entry point bm25_search — H2D of the
     # query batch, the search, D2H of the [Q, k] results — timed per call
@@ -236,10 +266,14 @@ def main():
                "batches": args.e2e_batches,
                "what": "bm25_search host buffers: H2D queries -> search -> D2H docs+scores, "
                        "host clock around the synchronous call"}
+    nnz_total = int(indptr[-1])
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+        z = torch.tensor([nnz_total], dtype=torch.int64, device=dev)
+        dist.all_reduce(z)  # the realised postings of every rank's shard
+        nnz_total = int(z.item())
 
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     qps = Q * args.steps / elapsed
@@ -248,7 +282,7 @@ def main():
     kern_ms = prof["score_ms"] / max(prof["score_launches"], 1)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     shift = int(np.log2(info["tile_docs"]))
-    traffic = load_traffic(args.traffic, args.config, shift) if world == 1 else None
+    traffic = load_traffic(args.traffic, args.config, shift, T) if world == 1 else None
 
     if rank == 0:
         out = {
@@ -269,13 +303,18 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded Zipf CSC index + df^0.75 queries, csrc/synth.cpp)",
             "config": {
-                "workload": f"{args.config}: {cfg.name}" + (
+                "workload": f"{args.config}: {cfg.name}, {T} terms per query" + (
                     f"; one rank's doc shard [{lo}, {hi}) of the 8-GPU job" if emul else ""),
                 "segments": "sparse" if info.get("sparse") else "dense",
-                "n_docs": cfg.n_docs, "n_terms": cfg.n_terms, "nnz": int(indptr[-1]) if world == 1
-                else cfg.nnz, "batch": Q, "terms_per_query": T, "k": k,
+                "n_docs": cfg.n_docs, "n_terms": cfg.n_terms, "nnz": nnz_total,
+                "batch": Q, "terms_per_query": T, "k": k,
                 "tile_docs": info["tile_docs"],
-                "parallelism": f"doc-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                "parallelism": f"doc-shard x{world}" + (
+                    f" + {'RCCL' if args.backend == 'nccl' else args.backend} all-gathers "
+                    "(sample keys, packed [Q, k] lists)" if world > 1 else ""),
+                "score_kernels": sorted(dispatch["kernels"]),
+                "term_lanes": dispatch["term_lanes"],
+                "tiles_per_item": dispatch["band_tiles"],
             },
             "roofline": {
                 "bound": "hbm",
@@ -286,9 +325,11 @@ def main():
                 "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
                 "traffic_source": (f"profiles/traffic.json: {traffic.get('method')}; "
                                    f"L2 hit rate {traffic.get('l2_hit_rate')}") if traffic else None,
-                "kernel": "score_tiles",
+                "kernel": "score pass (score_flat_kernel SAMPLE + theta_wave_kernel + "
+                          "score_flat_kernel REST)",
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
+                "scope": "rank 0's shard" if world > 1 else "the whole index",
             },
             "cpu_baseline": cpu,
             "e2e": e2e,

@@ -133,7 +133,7 @@ int bm25_max_token_device(bm25_index* idx, const int32_t* d_queries, int64_t Q,
  * score matrix (term-major, doc ids ascending per term = what
  * bm25_index_create and the bm25s on-disk format hold).
  * Replaces: the scoring half of the bm25s writer that produced the
- *           reference's index (animal_index_bm25/*, params.index.json:1-11,
+ *           reference's index (animal_index_bm25/, params.index.json:1-11,
  *           bm25_test.py:19-38; method 0) and BM25.fit's matrix
  *           (bm25.py:30-121; method 1).
  *   docs/terms [n] int32, tfs [n] f32 (> 0), any order, one triple per
@@ -268,6 +268,43 @@ int bm25_profile_read(bm25_index* idx, double* score_ms_total,
  */
 int bm25_search_stats(bm25_index* idx, int64_t* rescored_tiles,
                       int64_t* fallback_queries);
+
+/*
+ * Search options of one handle.  A new handle takes them from the
+ * environment (BM25_FLAT, BM25_FLAT_BW, BM25_ITEMS_PER_WAVE, BM25_SAMPLE_P,
+ * BM25_LIST_CAP, BM25_CLAIM_CH, BM25_CLAIM_M) at bm25_index_create; these
+ * calls change or read them afterwards, effective from the next search.
+ * Results never depend on them (every setting is bit-exact); they choose
+ * kernels and geometry:
+ *   "flat"           1 (default): the flat score kernel for queries of 1..64
+ *                    terms; 0: score_wave_kernel for every phase
+ *   "flat_bw"        tiles per flat-kernel item: 0 = automatic, 1, 2, 4, 8
+ *   "items_per_wave" automatic flat_bw: halved while a phase gives the
+ *                    resident waves fewer items each (default 8)
+ *   "sample_p"       largest sampling stride, a power of two (default 8;
+ *                    1 = no threshold: the exact pass over every tile)
+ *   "list_cap"       candidate-list capacity per query (0 = automatic; small
+ *                    values force queries through the exact fallback stage)
+ *   "claim_ch", "claim_m"  flat-kernel item claims: items per claim (1),
+ *                    counters per XCD (4)
+ * Replaces no reference call (the reference has no tuning surface; its MAX
+ * custom op takes compile-time parameters, graph.py:72).
+ */
+int bm25_index_set_option(bm25_index* idx, const char* name, int64_t value);
+int bm25_index_get_option(const bm25_index* idx, const char* name, int64_t* value);
+
+/*
+ * What the last search on the handle launched (diagnostics, no device wait):
+ *   *kernels     bit mask of score kernels: 1 flat SAMPLE, 2 flat REST,
+ *                4 flat ALL (exact pass / fallback stage), 8 wave SAMPLE,
+ *                16 wave REST, 32 wave ALL
+ *   *term_lanes  flat kernel: term lanes per tile (8, 16, 32 or 64)
+ *   band_tiles   [3]: flat kernel tiles per item of ALL, SAMPLE, REST
+ *   *sample_p    sampling stride of the search (1: exact pass)
+ * Any pointer may be NULL.
+ */
+int bm25_search_dispatch(bm25_index* idx, uint32_t* kernels, int32_t* term_lanes,
+                         int32_t* band_tiles, int32_t* sample_p);
 
 #ifdef __cplusplus
 }

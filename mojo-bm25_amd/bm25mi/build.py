@@ -43,8 +43,12 @@ def build(force: bool = False, verbose: bool = False) -> None:
     os.makedirs(objdir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
              "-Wno-unused-value"]
+    srcs = [os.path.join(CSRC, src) for src in HIP_SOURCES]
+    # the library travels without its objects (.gpurunignore): up to date when
+    # newer than every source and header
+    lib_fresh = not force and not _stale(lib, srcs + hdrs)
     objs, jobs = [], []
-    for src in HIP_SOURCES:
+    for src in ([] if lib_fresh else HIP_SOURCES):
         o = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
         objs.append(o)
         if force or _stale(o, [os.path.join(CSRC, src)] + hdrs):
@@ -55,7 +59,7 @@ def build(force: bool = False, verbose: bool = False) -> None:
             list(ex.map(lambda c: _run(c, verbose), jobs))
         for c in jobs:
             os.replace(c[-2], c[-2][:-4])
-    if force or jobs or _stale(lib, objs):
+    if not lib_fresh and (force or jobs or _stale(lib, objs)):
         tmp = lib + ".tmp"
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, verbose)
         os.replace(tmp, lib)

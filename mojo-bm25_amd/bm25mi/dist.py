@@ -1,7 +1,7 @@
 """Doc-sharded search across ranks.
 
 One process per GPU.  Rank r owns the contiguous document range
-``synth.shard_bounds(N, W, r)`` as an independent index whose ``doc_offset``
+``shard_bounds(N, W, r)`` (bm25mi.shard) as an independent index whose ``doc_offset``
 is the global id of its first document, and searches the whole (replicated)
 query batch on it.  The path has two exchanges, both all-gathers (RCCL over
 xGMI with the ``nccl`` backend): every rank's sample keys (global doc ids),
@@ -19,25 +19,10 @@ from typing import Callable, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from .shard import shard_bounds  # noqa: F401  (the one definition; re-exported here)
+
 # merge(g_docs [W,Q,k] int32, g_scores [W,Q,k] f32) -> (docs [Q,k], scores [Q,k])
 MergeFn = Callable[[torch.Tensor, torch.Tensor], Tuple[torch.Tensor, torch.Tensor]]
-
-
-def shard_bounds(n_docs: int, world: int, rank: int, align: int = 2048) -> Tuple[int, int]:
-    """Contiguous doc range [lo, hi) of ``rank``: an even split with inner
-    boundaries rounded to multiples of ``align`` (the 2048-doc LDS tile, so no
-    shard carries a partial tile except the last; synth.shard_bounds uses the
-    generator's 16384-doc chunks, a multiple of it)."""
-    if world < 1 or not 0 <= rank < world:
-        raise ValueError(f"bad shard {rank} of {world}")
-
-    def b(r: int) -> int:
-        if r >= world:
-            return int(n_docs)
-        x = (int(n_docs) * r) // world
-        return min(int(n_docs), (x + align // 2) // align * align)
-
-    return b(rank), b(rank + 1)
 
 
 def _all_gather(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
@@ -88,6 +73,23 @@ def gpu_merge(device: int, stream=None) -> MergeFn:
     return merge
 
 
+def _global_docs(index, device, group=None) -> int:
+    """Documents of the whole collection: the sum of every rank's shard,
+    all-reduced once and cached on the index object."""
+    n = getattr(index, "_bm25_global_docs", None)
+    if n is None:
+        if dist.get_world_size(group) == 1:
+            n = int(index.n_docs)
+        else:
+            backend = dist.get_backend(group)
+            t = torch.tensor([int(index.n_docs)], dtype=torch.int64,
+                             device="cpu" if backend == "gloo" else device)
+            dist.all_reduce(t, group=group)
+            n = int(t.item())
+        index._bm25_global_docs = n
+    return n
+
+
 def gather_keys(keys: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
     """All ranks' [Q, S] sample keys -> [W, Q, S] (rank-major), on every rank."""
     return _all_gather(keys, group)
@@ -97,7 +99,8 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
                    d_docs: torch.Tensor, d_scores: torch.Tensor,
                    merge: Optional[MergeFn] = None, stream=None,
                    group: Optional[dist.ProcessGroup] = None,
-                   exchange: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
+                   exchange: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
+                   n_docs_total: Optional[int] = None
                    ) -> Tuple[torch.Tensor, torch.Tensor]:
     """One rank's doc-sharded search with a GLOBAL threshold (bm25_search_
     sample/finish_device): this shard's sample keys are all-gathered, theta =
@@ -110,15 +113,27 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
     key all-gather (tests).
 
     Everything — kernels and collectives — is enqueued on ``stream`` (default:
-    the current stream): the collectives order against torch's current
-    stream, so the body runs with ``stream`` made current."""
+    the current stream; a torch.cuda.Stream or a raw hipStream_t handle): the
+    collectives order against torch's current stream, so the body runs with
+    ``stream`` made current.
+
+    ``k`` is checked against the whole collection's document count, as the
+    single-index search checks it (numpy's argpartition error,
+    bm25_native.py:205): ``n_docs_total``, or one all-reduce of the shards'
+    counts on the first search (cached on ``index``)."""
     if stream is None:
         stream = torch.cuda.current_stream(d_queries.device)
+    elif not isinstance(stream, torch.cuda.Stream):
+        stream = torch.cuda.ExternalStream(int(stream), device=d_queries.device)
     with torch.cuda.stream(stream):
         world = dist.get_world_size(group) if exchange is None else None
         Q = d_queries.shape[0]
         if exchange is not None:
             world = int(exchange.world)  # type: ignore[attr-defined]
+        total = n_docs_total if n_docs_total is not None else (
+            _global_docs(index, d_queries.device, group) if exchange is None else None)
+        if total is not None and k > total:
+            raise ValueError(f"kth(={total - k}) out of bounds ({total})")
         S = index.sample_width(k, world, shard_docs_max)
         # S > 0: the sample pass zeroes the keys itself (zero_search_kernel)
         keys = (torch.empty if S > 0 else torch.zeros)((Q, max(S, 1)), dtype=torch.int64,
@@ -142,6 +157,8 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
         index.search_finish_device(d_queries, k, world, shard_docs_max, all_keys, pk[0],
                                    pk[1].view(torch.float32), stream)
         g = _all_gather(pk, group)  # [W, 2, Q, k]: one collective for docs and scores
+        # the merge reads rank w's docs at w * 2Qk and its scores Qk later
+        assert tuple(g.shape) == (world, 2, Q, k) and g.is_contiguous(), tuple(g.shape)
         from .index import merge_sorted_device
         merge_sorted_device(d_queries.device.index, g, g[:, 1].view(torch.float32), world, Q, k,
                             2 * Q * k, d_docs, d_scores, stream)

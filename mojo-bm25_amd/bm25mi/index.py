@@ -27,7 +27,7 @@ class GpuIndex:
     index (indptr/indices/data ``.csc.index.npy``)."""
 
     def __init__(self, indptr, indices, data, n_docs: int, device: int = 0,
-                 doc_offset: int = 0):
+                 doc_offset: int = 0, options: Optional[dict] = None):
         indptr = np.asarray(indptr)
         if indptr.ndim != 1 or indptr.size < 1:
             raise ValueError("indptr must be a 1-D array of n_terms + 1 offsets")
@@ -51,6 +51,8 @@ class GpuIndex:
         self._h = h
         # the device holds its own copy
         self._indptr = self._indices = self._data = None
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
 
     # ------------------------------------------------------------------
     @classmethod
@@ -184,6 +186,35 @@ class GpuIndex:
                                     ctypes.byref(ns), ctypes.byref(rs)))
         return {"score_ms": sm.value, "score_launches": sl.value, "total_ms": tm.value,
                 "searches": ns.value, "rescored_tiles_last": rs.value}
+
+    # ------------------------------------------------------------------
+    def set_option(self, name: str, value: int) -> None:
+        """A search option of this handle (bm25_index_set_option: flat,
+        flat_bw, items_per_wave, sample_p, list_cap, claim_ch, claim_m)."""
+        check(lib.bm25_index_set_option(self._h, name.encode(), int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        check(lib.bm25_index_get_option(self._h, name.encode(), ctypes.byref(v)))
+        return v.value
+
+    KERNELS = {1: "flat_sample", 2: "flat_rest", 4: "flat_all", 8: "wave_sample",
+               16: "wave_rest", 32: "wave_all"}
+
+    def last_dispatch(self) -> dict:
+        """What the last search launched (bm25_search_dispatch): the score
+        kernels by phase, the flat kernel's term lanes and tiles per item
+        (ALL, SAMPLE, REST) and the sampling stride."""
+        km = ctypes.c_uint32()
+        tl = ctypes.c_int32()
+        bt = (ctypes.c_int32 * 3)()
+        sp_ = ctypes.c_int32()
+        check(lib.bm25_search_dispatch(self._h, ctypes.byref(km), ctypes.byref(tl), bt,
+                                       ctypes.byref(sp_)))
+        return {"kernels": {n for b, n in self.KERNELS.items() if km.value & b},
+                "term_lanes": tl.value,
+                "band_tiles": {"all": bt[0], "sample": bt[1], "rest": bt[2]},
+                "sample_p": sp_.value}
 
     def search_stats(self) -> dict:
         """Selection statistics of the last search: tiles re-scored exactly,

@@ -8,7 +8,8 @@ bounded column blocks, so the global arrays are never copied whole; the shard
 is an ordinary CSC with local doc ids (int32) and its own int64 ``indptr``.
 ``load_bm25s_shard`` does this straight from a bm25s directory.
 
-The bounds are dist.shard_bounds' (2048-doc aligned), the same on every rank.
+``shard_bounds`` is the one definition of the per-rank doc ranges (2048-doc
+aligned, the same on every rank); bm25mi.dist and bm25mi.synth use it.
 """
 from __future__ import annotations
 
@@ -21,8 +22,9 @@ BLOCK_POSTINGS = 1 << 26
 
 
 def shard_bounds(n_docs: int, world: int, rank: int, align: int = 2048) -> Tuple[int, int]:
-    """Contiguous doc range [lo, hi) of ``rank`` (dist.shard_bounds' rule,
-    without importing torch)."""
+    """Contiguous doc range [lo, hi) of ``rank``: an even split with inner
+    boundaries rounded to multiples of ``align`` (the 2048-doc LDS tile, so no
+    shard carries a partial tile except the last)."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"bad shard {rank} of {world}")
 

@@ -106,10 +106,8 @@ def make_queries(cfg: Config, df: Optional[np.ndarray] = None, n_queries: Option
 
 
 def shard_bounds(n_docs: int, world: int, rank: int, align: int = 16384):
-    """Contiguous doc range of a shard, aligned to the generator's chunks."""
-    def b(r):
-        if r >= world:
-            return n_docs
-        x = (n_docs * r) // world
-        return min(n_docs, (x + align // 2) // align * align)
-    return b(rank), b(rank + 1)
+    """Contiguous doc range of a shard (bm25mi.shard.shard_bounds' rule),
+    aligned to the generator's 16384-doc chunks (a multiple of the 2048-doc
+    tile) so that a shard is generated independently of the others."""
+    from .shard import shard_bounds as bounds
+    return bounds(n_docs, world, rank, align=align)

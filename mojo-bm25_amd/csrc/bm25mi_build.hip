@@ -80,8 +80,8 @@ template <int METHOD>
 __global__ __launch_bounds__(256) void score_postings_kernel(
     const uint64_t* __restrict__ keys, const uint32_t* __restrict__ ord,
     const float* __restrict__ tfs, const int32_t* __restrict__ doc_len,
-    const float* __restrict__ idf, int64_t n, double avgdl, double k1, double b,
-    int32_t* __restrict__ out_indices, float* __restrict__ out_data,
+    const float* __restrict__ idf, int64_t n, int64_t n_docs, int64_t n_terms, double avgdl,
+    double k1, double b, int32_t* __restrict__ out_indices, float* __restrict__ out_data,
     double* __restrict__ out_data64) {
 #pragma clang fp contract(off)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -90,8 +90,9 @@ __global__ __launch_bounds__(256) void score_postings_kernel(
     const int32_t doc = (int32_t)(uint32_t)k;
     const uint32_t term = (uint32_t)(k >> 32);
     const float tf = tfs[ord[i]];
-    const float w = idf[term];
-    const int32_t dl = doc_len[doc];
+    const bool ok = doc >= 0 && (int64_t)doc < n_docs && (int64_t)term < n_terms;  // (checked
+    const float w = ok ? idf[term] : 0.f;                                        // by the host)
+    const int32_t dl = ok ? doc_len[doc] : 0;
     float v32;
     double v64;
     if (METHOD == kLucene) {
@@ -165,6 +166,12 @@ hipError_t build_scores(int64_t n_docs, int64_t n_terms, int64_t n, const int32_
     hipLaunchKernelGGL(pack_keys_kernel, dim3(grid_for(n)), dim3(256), 0, st, d_docs, d_terms,
                        d_tfs, n, n_docs, n_terms, keys, ord, d_err);
     BTRY(hipGetLastError());
+    // ids out of range stop the build here: the scoring pass indexes doc_len
+    // and idf with them (the caller reports d_err as EINVAL)
+    int32_t herr = 0;
+    BTRY(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    BTRY(hipStreamSynchronize(st));
+    if (herr & 1) return done(hipSuccess);
     hipcub::DoubleBuffer<uint64_t> kb(keys, keys2);
     hipcub::DoubleBuffer<uint32_t> ob(ord, ord2);
     BTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, kb, ob, (int)n, 0, end_bit, st));
@@ -189,10 +196,12 @@ hipError_t build_scores(int64_t n_docs, int64_t n_terms, int64_t n, const int32_
     }
     if (method == kLucene)
       hipLaunchKernelGGL(score_postings_kernel<kLucene>, dim3(grid_for(n)), dim3(256), 0, st, sk,
-                         so, d_tfs, d_doc_len, w, n, avgdl, k1, b, d_indices, d_data, d_data64);
+                         so, d_tfs, d_doc_len, w, n, n_docs, n_terms, avgdl, k1, b, d_indices, d_data,
+                         d_data64);
     else
       hipLaunchKernelGGL(score_postings_kernel<kBm25Py>, dim3(grid_for(n)), dim3(256), 0, st, sk,
-                         so, d_tfs, d_doc_len, w, n, avgdl, k1, b, d_indices, d_data, d_data64);
+                         so, d_tfs, d_doc_len, w, n, n_docs, n_terms, avgdl, k1, b, d_indices, d_data,
+                         d_data64);
     BTRY(hipGetLastError());
     BTRY(hipcub::DeviceScan::ExclusiveSum(tmp, b2, df, (unsigned long long*)d_indptr,
                                           (int)(n_terms + 1), st));

@@ -77,6 +77,7 @@ struct bm25_index {
   hipEvent_t ws_done = nullptr;    // end of the last search that used the workspace
   hipStream_t ws_stream = nullptr; // its stream
   int32_t* d_maxtok = nullptr;     // bm25_max_token_device result
+  bool sampled = false;            // a sample half ran since the last finish half
 };
 
 namespace {
@@ -99,23 +100,90 @@ void free_ws(Workspace& ws) {
 
 // Candidate-list capacity per query: the keys above theta of the non-sample
 // tiles number about (P-1)*k; a list that overflows sends its query to the
-// exact fallback stage (BM25_LIST_CAP overrides, for tests).
-int32_t list_cap_for(int64_t k) {
-  const int e = env_int("BM25_LIST_CAP", 0);
-  if (e > 0) return e;
+// exact fallback stage (the list_cap option overrides, for tests).
+int32_t list_cap_for(const SearchOpts& o, int64_t k) {
+  if (o.list_cap > 0) return o.list_cap;
   return (int32_t)std::min<int64_t>(65536, std::max<int64_t>(2048, 64 * k));
 }
 
+// Options of a new handle: the BM25_* environment (include/bm25mi.h).
+SearchOpts env_opts() {
+  SearchOpts o;
+  o.flat = env_int("BM25_FLAT", o.flat) != 0;
+  o.flat_bw = env_int("BM25_FLAT_BW", o.flat_bw);
+  o.items_per_wave = env_int("BM25_ITEMS_PER_WAVE", o.items_per_wave);
+  o.sample_p = env_int("BM25_SAMPLE_P", o.sample_p);
+  o.list_cap = env_int("BM25_LIST_CAP", o.list_cap);
+  o.claim_ch = env_int("BM25_CLAIM_CH", o.claim_ch);
+  o.claim_m = env_int("BM25_CLAIM_M", o.claim_m);
+  return o;
+}
+
+// Sets one option (EINVAL names the accepted values).
+int set_opt(SearchOpts& o, const char* name, int64_t v) {
+  auto is_pow2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
+  if (!name) return fail(BM25_EINVAL, "NULL option name");
+  const std::string n = name;
+  if (n == "flat") {
+    if (v != 0 && v != 1) return fail(BM25_EINVAL, "flat must be 0 or 1");
+    o.flat = (int)v;
+  } else if (n == "flat_bw") {
+    if (v != 0 && !(is_pow2(v) && v <= 8)) return fail(BM25_EINVAL, "flat_bw must be 0, 1, 2, 4 or 8");
+    o.flat_bw = (int)v;
+  } else if (n == "items_per_wave") {
+    if (v < 1 || v > 1024) return fail(BM25_EINVAL, "items_per_wave must be in 1..1024");
+    o.items_per_wave = (int)v;
+  } else if (n == "sample_p") {
+    if (!is_pow2(v) || v > 64) return fail(BM25_EINVAL, "sample_p must be a power of two in 1..64");
+    o.sample_p = (int)v;
+  } else if (n == "list_cap") {
+    if (v < 0 || v > (1 << 20)) return fail(BM25_EINVAL, "list_cap must be in 0..2^20");
+    o.list_cap = (int)v;
+  } else if (n == "claim_ch") {
+    if (v < 1 || v > 64) return fail(BM25_EINVAL, "claim_ch must be in 1..64");
+    o.claim_ch = (int)v;
+  } else if (n == "claim_m") {
+    if (v < 1 || v > kClaimM) return fail(BM25_EINVAL, "claim_m must be in 1..%d", kClaimM);
+    o.claim_m = (int)v;
+  } else {
+    return fail(BM25_EINVAL, "unknown option '%s'", name);
+  }
+  return BM25_OK;
+}
+
+int get_opt(const SearchOpts& o, const char* name, int64_t* v) {
+  if (!name || !v) return fail(BM25_EINVAL, "NULL argument");
+  const std::string n = name;
+  if (n == "flat") *v = o.flat;
+  else if (n == "flat_bw") *v = o.flat_bw;
+  else if (n == "items_per_wave") *v = o.items_per_wave;
+  else if (n == "sample_p") *v = o.sample_p;
+  else if (n == "list_cap") *v = o.list_cap;
+  else if (n == "claim_ch") *v = o.claim_ch;
+  else if (n == "claim_m") *v = o.claim_m;
+  else return fail(BM25_EINVAL, "unknown option '%s'", name);
+  return BM25_OK;
+}
+
 int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
-  (void)T;
   Workspace& ws = h->ws;
-  if (Q <= ws.cap_q && k <= ws.cap_k) return BM25_OK;
+  const int64_t need_seg = seg_entries(h->ix, std::max(Q, ws.cap_q), T);
+  if (Q <= ws.cap_q && k <= ws.cap_k) {
+    if (need_seg <= ws.cap_seg) return BM25_OK;
+    // a wider query batch on a sparse index: only the segment table grows
+    hipFree(ws.seg);
+    ws.seg = nullptr;
+    ws.cap_seg = 0;
+    HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * need_seg), "hipMalloc(seg)");
+    ws.cap_seg = need_seg;
+    return BM25_OK;
+  }
   const int64_t q = std::max(Q, ws.cap_q);
   const int64_t kk = std::max<int64_t>(k, ws.cap_k);
   free_ws(ws);
   const int64_t nt = h->ix.ntiles;
   const int64_t mf = maxflag_for((int)kk, nt);
-  const int32_t C = list_cap_for(kk);
+  const int32_t C = list_cap_for(h->ix.opt, kk);
   HIP_TRY(hipMalloc(&ws.cand, sizeof(uint64_t) * q * nt * kTileM), "hipMalloc(cand)");
   HIP_TRY(hipMalloc(&ws.theta, sizeof(uint64_t) * q), "hipMalloc(theta)");
   HIP_TRY(hipMalloc(&ws.list, sizeof(uint64_t) * q * C), "hipMalloc(list)");
@@ -128,7 +196,7 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
   HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * 4), "hipMemset(counters)");
   HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMalloc(wctr)");
-  ws.cap_seg = seg_entries(h->ix, q);
+  ws.cap_seg = need_seg;
   if (ws.cap_seg > 0) HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * ws.cap_seg), "hipMalloc(seg)");
   ws.list_cap = C;
   ws.cap_q = q;
@@ -206,25 +274,15 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   int rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
+  const int P = sample_geom(h->ix.ntiles, k, 1, h->ix.opt.sample_p).P;
+  h->ix.disp = Dispatch{};
+  h->ix.disp.sample_p = P;
   EventPair* ev = next_events(h);
   if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
   HIP_TRY(launch_score(h->ix, d_queries, Q, T, k, h->ws, st), "score launch");
   if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
-  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, sample_geom(h->ix.ntiles, k, 1).P, h->ws,
-                        d_docs, d_scores, st), "select launch");
-  if (env_int("BM25_DEBUG_LISTS", 0)) {  // dev diagnostic: candidate-list sizes
-    std::vector<int32_t> c(Q);
-    hipStreamSynchronize(st);
-    hipMemcpy(c.data(), h->ws.list_cnt, sizeof(int32_t) * Q, hipMemcpyDeviceToHost);
-    double sum = 0;
-    int32_t mx = 0;
-    for (int32_t x : c) {
-      sum += x;
-      mx = std::max(mx, x);
-    }
-    fprintf(stderr, "lists: mean %.1f max %d cap %d\n", sum / std::max<int64_t>(Q, 1), mx,
-            h->ws.list_cap);
-  }
+  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, P, h->ws, d_docs, d_scores, st),
+          "select launch");
   if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
   HIP_TRY(hipEventRecord(h->ws_done, st), "hipEventRecord");
   if (h->prof) {
@@ -295,8 +353,7 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     if (ip[t + 1] - ip[t] > n_docs)
       return fail(BM25_EINVAL, "column %lld has more entries than n_docs", (long long)t);
   }
-  int shift = env_int("BM25_TILE_SHIFT", kDefaultTileShift);
-  if (!tile_shift_supported(shift)) return fail(BM25_EINVAL, "BM25_TILE_SHIFT=%d not compiled (10..11)", shift);
+  const int shift = kDefaultTileShift;
   const int64_t ntiles = (n_docs + (1LL << shift) - 1) >> shift;
   if (ntiles > 65536) return fail(BM25_EINVAL, "n_docs=%lld needs %lld tiles (> 65536)", (long long)n_docs, (long long)ntiles);
 
@@ -308,6 +365,7 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
 
   bm25_index* h = new bm25_index();
   DevIndex& ix = h->ix;
+  ix.opt = env_opts();
   ix.device = device;
   ix.n_docs = n_docs;
   ix.n_terms = n_terms;
@@ -515,7 +573,7 @@ int bm25_max_token_device(bm25_index* h, const int32_t* d_queries, int64_t Q, in
 static SampleGeom shard_geom(const bm25_index* h, int64_t shard_docs_max, int32_t world, int k) {
   const int64_t D = 1ll << h->ix.tile_shift;
   const int64_t nt = std::max<int64_t>((std::max<int64_t>(shard_docs_max, h->ix.n_docs) + D - 1) / D, 1);
-  return sample_geom(nt, k, std::max(world, 1));
+  return sample_geom(nt, k, std::max(world, 1), h->ix.opt.sample_p);
 }
 
 int bm25_sample_width(const bm25_index* h, int64_t shard_docs_max, int32_t world, int32_t k,
@@ -543,6 +601,9 @@ int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   h->split_ev = next_events(h);
   if (h->split_ev) HIP_TRY(hipEventRecord(h->split_ev->a, st), "hipEventRecord");
   const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
+  h->ix.disp = Dispatch{};
+  h->ix.disp.sample_p = g.P;
+  h->sampled = true;
   HIP_TRY(launch_sample(h->ix, d_queries, Q, T, g, d_keys, h->ws, st), "sample launch");
   return BM25_OK;
 }
@@ -563,6 +624,11 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   const hipStream_t st = (hipStream_t)stream;
   HIP_TRY(order_ws(h, st), "workspace order");
   const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
+  if (!h->sampled) {  // no sample half ran for this search (S = 0)
+    h->ix.disp = Dispatch{};
+    h->ix.disp.sample_p = g.P;
+  }
+  h->sampled = false;
   HIP_TRY(launch_finish(h->ix, d_queries, Q, T, k, g, world, d_all_keys, h->ws, st),
           "finish launch");
   EventPair* ev = h->split_ev;
@@ -747,6 +813,38 @@ int bm25_search_stats(bm25_index* h, int64_t* rescored_tiles, int64_t* fallback_
   read_counters(h, cnt);
   if (rescored_tiles) *rescored_tiles = cnt[3];
   if (fallback_queries) *fallback_queries = cnt[2];
+  return BM25_OK;
+}
+
+int bm25_index_set_option(bm25_index* h, const char* name, int64_t value) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  std::lock_guard<std::mutex> lk(h->mu);
+  const int old_cap = h->ix.opt.list_cap;
+  const int rc = set_opt(h->ix.opt, name, value);
+  if (rc) return rc;
+  if (h->ix.opt.list_cap != old_cap && h->ws.cap_q > 0) {  // the list capacity is sized in
+    hipSetDevice(h->ix.device);                            // the workspace: rebuild it
+    if (h->ws_done) hipEventSynchronize(h->ws_done);
+    free_ws(h->ws);
+  }
+  return BM25_OK;
+}
+
+int bm25_index_get_option(const bm25_index* h, const char* name, int64_t* value) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  return get_opt(h->ix.opt, name, value);
+}
+
+int bm25_search_dispatch(bm25_index* h, uint32_t* kernels, int32_t* term_lanes,
+                         int32_t* band_tiles, int32_t* sample_p) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  std::lock_guard<std::mutex> lk(h->mu);
+  const Dispatch& d = h->ix.disp;
+  if (kernels) *kernels = d.kernels;
+  if (term_lanes) *term_lanes = d.term_lanes;
+  if (band_tiles)
+    for (int i = 0; i < 3; ++i) band_tiles[i] = d.band_tiles[i];
+  if (sample_p) *sample_p = d.sample_p;
   return BM25_OK;
 }
 

@@ -44,24 +44,44 @@ constexpr int kMaxK = 4096;
 constexpr int kMergeP = 8192;
 // Posting arrays carry a small tail (so posting 0 exists for an empty index).
 constexpr int64_t kPostingPad = 64;
-// Default tile: 2^11 = 2048 docs, one wavefront's LDS accumulator (8 KB).
+// Tile: 2^11 = 2048 docs, one wavefront's LDS accumulator (8 KB).
 constexpr int kDefaultTileShift = 11;
 
-// Item claims of the pipelined score kernel (bm25mi_kernels.hip): items per
-// claim, counters per XCD, int32 stride between counters (256 B).
-constexpr int kClaimCH = 8;
-constexpr int kClaimM = 8;  // counters allocated per XCD (4 used by default)
+// Item claims of the flat score kernel (bm25mi_kernels.hip): counters per
+// XCD (allocated), int32 stride between counters (256 B).
+constexpr int kClaimM = 8;
 constexpr int kCtrStride = 64;
-// Item order of the pipelined score kernel: bands of kBand consecutive tiles,
-// query by query inside a band; sample tiles in groups of kSampleGroup.
-constexpr int kBand = 8;
-#ifndef BM25_BANDW  // tiles per band item of the band kernel (4 or 8)
-#define BM25_BANDW 8
-#endif
-constexpr int kSampleGroup = BM25_BANDW;
+// Sample tiles come in groups of kSampleGroup consecutive tiles (sample_geom).
+constexpr int kSampleGroup = 8;
 constexpr int kWctrInts = 8 * kClaimM * kCtrStride;
 // Claim-counter regions of a search: SAMPLE, REST (or the exact pass), fallback.
 constexpr int kWctrRegions = 3;
+
+// Search dispatch options of one index handle: a snapshot of the BM25_*
+// environment at bm25_index_create, changed by bm25_index_set_option
+// (include/bm25mi.h lists the names).  Read per search — never cached in
+// function statics — so every option takes effect on the next search.
+struct SearchOpts {
+  int flat = 1;            // 0: score_wave_kernel for every phase
+  int flat_bw = 0;         // tiles per flat item: 0 = auto, else 1, 2, 4 or 8
+  int items_per_wave = 8;  // auto flat_bw: halve while a phase gives fewer items per wave
+  int sample_p = 8;        // largest sampling stride (1: the exact pass over every tile)
+  int list_cap = 0;        // candidate-list capacity per query (0: auto)
+  int claim_ch = 1;        // flat items per claim
+  int claim_m = 4;         // claim counters per XCD (1..kClaimM)
+};
+
+// What the last search launched (bm25_search_dispatch).
+enum {
+  kKFlatSample = 1, kKFlatRest = 2, kKFlatAll = 4,
+  kKWaveSample = 8, kKWaveRest = 16, kKWaveAll = 32,
+};
+struct Dispatch {
+  uint32_t kernels = 0;       // kK* bits of the score kernels launched
+  int32_t term_lanes = 0;     // flat kernel: term lanes per tile (8, 16, 32, 64)
+  int32_t band_tiles[3] = {0, 0, 0};  // flat kernel: tiles per item of ALL, SAMPLE, REST
+  int32_t sample_p = 0;       // sampling stride (1: exact pass)
+};
 
 struct DevIndex {
   int device = 0;
@@ -84,6 +104,8 @@ struct DevIndex {
   int64_t n_pairs = 0;
   uint16_t* ldoc = nullptr;
   float* val = nullptr;
+  SearchOpts opt;
+  mutable Dispatch disp;  // written by the launchers (callers hold the handle's mutex)
 };
 
 struct Workspace {
@@ -101,8 +123,8 @@ struct Workspace {
   int32_t* counters = nullptr;   // [0]/[1] rescore queue length / pop cursor,
                                  // [2] fallback queries, [3] tiles re-scored this search
   int32_t* wctr = nullptr;       // [kWctrRegions][kWctrInts] item-claim counters, zeroed per search
-  uint64_t* seg = nullptr;       // sparse index: [Q][bands][64] segment of (tile, term) lanes of
-                                 // each band item (start | len << 32), built per search
+  uint64_t* seg = nullptr;       // sparse index: [Q][tiles/8][TT][8] segment of each (query,
+                                 // term position, tile) (start | len << 32), built per search
   int64_t cap_seg = 0;           // u64 entries of seg
 };
 
@@ -121,7 +143,7 @@ struct SampleGeom {
   int64_t S;
   int G;  // sample tiles come in groups of G consecutive tiles (bm25mi_kernels.hip)
 };
-SampleGeom sample_geom(int64_t ntiles, int k, int W);
+SampleGeom sample_geom(int64_t ntiles, int k, int W, int pmax);
 
 // Kernel launchers (bm25mi_kernels.hip).  All enqueue on `stream`.
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,
@@ -132,8 +154,9 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,
 hipError_t launch_count_tiles(const DevIndex& ix, const int32_t* d_indices, int64_t* d_cnt,
                               int32_t* d_err, hipStream_t stream);
 hipError_t launch_fill_tiles(const DevIndex& ix, const int32_t* d_indices, hipStream_t stream);
-// u64 entries of Workspace::seg a search of Q queries needs (0: dense index).
-int64_t seg_entries(const DevIndex& ix, int64_t Q);
+// u64 entries of Workspace::seg a search of Q queries of T terms needs (0:
+// dense index, or a search the flat kernel does not serve).
+int64_t seg_entries(const DevIndex& ix, int64_t Q, int64_t T);
 // Score pass of a single-index search: SAMPLE + theta + REST (or the exact
 // pass when the index is too small to sample).
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,

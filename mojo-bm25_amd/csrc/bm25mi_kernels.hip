@@ -37,10 +37,7 @@ namespace bm25mi {
 
 enum Phase { kAll = 0, kSample = 1, kRest = 2 };
 
-#ifndef BM25_KJ
-#define BM25_KJ 8
-#endif
-constexpr int kJ = BM25_KJ;  // posting rows (64 postings each) in flight per wave
+constexpr int kJ = 8;       // posting rows (64 postings each) in flight per wave (add_group)
 constexpr int kWaves = 4;   // independent waves per score workgroup
 constexpr int kGroup = 64;  // query terms per descriptor group (one per lane)
 
@@ -56,18 +53,19 @@ struct IndexArgs {
   const int64_t* tl_ptr;    // sparse: tile lists
   const uint16_t* tl_tile;
   const uint32_t* tl_start;
-  const uint64_t* seg;      // sparse + band kernel: this search's per-item segments
+  const uint64_t* seg;      // sparse + flat kernel: this search's segment table
+  int64_t seg_zero;         // ... index of a zero entry past it
 };
 
 static IndexArgs args_of(const DevIndex& ix) {
   return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs,
                    ix.nnz, ix.doc_offset, ix.nonneg ? 1 : 0, ix.sparse ? 1 : 0, ix.tl_ptr,
-                   ix.tl_tile, ix.tl_start, nullptr};
+                   ix.tl_tile, ix.tl_start, nullptr, 0};
 }
 
 // Segment bounds [r0, r1) (relative to indptr[term]) of a valid term in a
 // tile.  Sparse: a binary search of the term's tile list (the cold paths; the
-// band kernel reads a per-search table instead, seg_table_kernel).
+// flat kernel reads a per-search table instead, seg_table_kernel).
 __device__ __forceinline__ void segment(const IndexArgs& a, int64_t term, int64_t tile,
                                         uint32_t& r0, uint32_t& r1) {
   if (!a.sparse) {
@@ -530,83 +528,6 @@ __device__ __forceinline__ int32_t tile_of32(uint32_t ti, uint32_t P, uint32_t G
 }
 
 
-// ---------------------------------------------------------------------------
-// Software-pipelined pieces of the scatter phase (score_pipe_kernel).  An
-// item's dependent loads — query terms -> (indptr, rel) -> postings — are
-// issued three, two and one items ahead of its adds, so the latency of each
-// level hides behind the work of the items in between.  Every stage issues a
-// fixed number of loads, none under a branch (lanes with nothing to load read
-// a valid dummy address), so the compiler's vmcnt waits stay counted instead
-// of draining the queue.
-// ---------------------------------------------------------------------------
-struct Desc {  // lane s < T: raw segment bounds of query term s
-  int64_t ip;
-  uint32_t r0, r1;
-  bool ok;
-};
-
-__device__ __forceinline__ Desc load_desc(const IndexArgs& a, int32_t term, int64_t tile) {
-  Desc d;
-  d.ok = term >= 0 && term < a.V;  // negative ids are padding (bm25_native.py:151)
-  const int64_t t = d.ok ? term : 0;
-  d.ip = a.indptr[t];
-  segment(a, t, tile, d.r0, d.r1);
-  return d;
-}
-
-// Inclusive prefix sum inside 16-lane rows (DPP row_shr; enough for T <= 16
-// because lanes >= T hold 0).
-__device__ __forceinline__ uint32_t scan16(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
-  return x;
-}
-
-// An item's posting rows: each query term's segment is cut into rows of 64
-// postings (one per lane), so a row belongs to one term and needs no term
-// mask.  Lane j of the table describes row j0 + j of the item.
-// (Rows aligned to 64-posting boundaries touch 3 cache lines instead of ~5 —
-// 271 M vs 307 M L1->L2 requests per config-3 REST pass — but add ~8 % rows
-// and more items past kJ rows: 5.64 vs 4.91 ms.)
-struct Rows {
-  int64_t base;    // posting index of the row's first posting (0 past the end)
-  uint32_t cnt;    // postings in the row (0: past the item's rows)
-  uint32_t term;   // the row's query term (T past the end)
-  uint32_t nrows;  // rows of the item (uniform)
-};
-
-__device__ __forceinline__ Rows make_rows(const Desc& d, int T, uint32_t j0) {
-  const uint32_t lane = lane_id();
-  const uint32_t len = ((int)lane < T && d.ok) ? d.r1 - d.r0 : 0u;
-  const int64_t beg = d.ip + (int64_t)d.r0;
-  const uint32_t nr = (len + 63u) >> 6;
-  const uint32_t rincl = T <= 16 ? scan16(nr) : wave_incl_scan(nr);
-  Rows r;
-  r.nrows = lane_u32(rincl, T - 1);
-  const uint32_t j = j0 + lane;  // the row this lane describes
-  // its term s = #{s < T : rincl[s] <= j}, by binary lifting over ds_bpermute
-  int pos = 0;
-#pragma unroll
-  for (int step = 64; step >= 1; step >>= 1) {
-    if (step > T) continue;  // uniform
-    const int c = pos + step;
-    const uint32_t x = (uint32_t)__shfl((int)rincl, min(c, T) - 1, 64);
-    if (c <= T && x <= j) pos = c;
-  }
-  const uint32_t st = (uint32_t)__shfl((int)(rincl - nr), pos, 64);
-  const uint32_t l = (uint32_t)__shfl((int)len, pos, 64);
-  const uint32_t blo = (uint32_t)__shfl((int)(uint32_t)beg, pos, 64);
-  const uint32_t bhi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)beg >> 32), pos, 64);
-  const uint32_t k = j - st;  // row index inside its term
-  const bool in = j < r.nrows;
-  r.base = in ? (int64_t)(((uint64_t)bhi << 32) | blo) + 64 * (int64_t)k : 0;
-  r.cnt = in ? min(64u, l - 64u * k) : 0u;
-  r.term = in ? (uint32_t)pos : (uint32_t)T;
-  return r;
-}
-
 // Buffer descriptors over the whole posting arrays (built once per kernel
 // from kernel arguments): a row's loads are then one scalar offset (its base)
 // plus the constant lane offset, with no per-lane address arithmetic.  Needs
@@ -624,227 +545,6 @@ __device__ __forceinline__ PostingRsrc posting_rsrc(const IndexArgs& a) {
   r.val = __builtin_amdgcn_make_buffer_rsrc((void*)a.val, 0, (int)((uint32_t)np * 4u), 0x00020000);
   return r;
 }
-
-// Loads of table rows [j0, j0 + kJ): slot + score per lane.  Lanes past a
-// row's postings read the next postings (or the zeroed pad after the last
-// one) and are masked by add_rows.  Every load is issued, so
-// the vmcnt waits stay counted.
-// (Giving the masked lanes an out-of-range buffer offset instead — no fetch —
-// made the config-3 score pass slower, 5.05 vs 4.77 ms, round 1.)
-template <int DIAG>
-__device__ __forceinline__ void issue_rows(const PostingRsrc& pr, const Rows& R, int j0,
-                                           uint32_t (&ld)[kJ], float (&v)[kJ]) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int j = 0; j < kJ; ++j) {
-    const uint32_t base = lane_u32((uint32_t)R.base, j0 + j);
-    ld[j] = __builtin_amdgcn_raw_buffer_load_b16(pr.ldoc, (int)(lane * 2u), (int)(base * 2u), 0);
-    v[j] = __uint_as_float(
-        __builtin_amdgcn_raw_buffer_load_b32(pr.val, (int)(lane * 4u), (int)(base * 4u), 0));
-  }
-}
-
-// Rows of a block processed: the first 4 or all kJ (a uniform choice from the
-// block's row count n); rows past n in the processed range are all-trash.
-__device__ __forceinline__ int rows_done(uint32_t n) { return n == 0 ? 0 : (n <= kJ / 2 ? kJ / 2 : kJ); }
-
-// Read-add-write of NR loaded rows, in order.  Lanes past a row's postings
-// are redirected to the lane's own trash slot (acc[2^S + lane], always 0) with
-// a zero score, so every LDS access runs unmasked (no exec-mask branches; the
-// compiler keeps its lgkmcnt waits counted); the redirected slots are written
-// back into ld for the sparse emission.  Each row is read, added and written
-// back before the next row of ANOTHER term is read — the LDS executes a
-// wave's instructions in order, so each doc's adds stay in query-term order
-// (scipy csc_matvec's sequence) — while the next row of the SAME term (distinct
-// docs) is read one row ahead.  (An LDS float atomic per row, ds_add_f32, ran
-// the config-3 score pass 4.7x slower: 24.8 vs 5.3 ms.)
-template <int S, int NR>
-__device__ __forceinline__ void rmw_rows(float* acc, const Rows& R, int j0, uint32_t (&ld)[kJ],
-                                         float (&v)[kJ], float th, uint64_t& hit) {
-  const uint32_t lane = lane_id();
-  const uint32_t trash = (1u << S) + lane;
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const bool m = lane < lane_u32(R.cnt, j0 + j);
-    ld[j] = m ? ld[j] : trash;
-    v[j] = m ? v[j] : 0.f;
-  }
-  // bit j of bm: row j0 + j starts a new term
-  const uint32_t tprev = (uint32_t)__shfl_up((int)R.term, 1, 64);
-  const uint32_t bm = (uint32_t)(__ballot(R.term != tprev) >> j0);
-  float x[NR];
-  x[0] = acc[ld[0]];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const bool same = j + 1 < NR && !((bm >> (j + 1)) & 1u);
-    if (same) x[j + 1] = acc[ld[j + 1]];
-    const float y = x[j] + v[j];
-    acc[ld[j]] = y;
-    hit |= __ballot(y >= th);  // th = NaN: never
-    if (j + 1 < NR && !same) x[j + 1] = acc[ld[j + 1]];
-  }
-}
-
-//
-// hit collects the lanes whose new running sum reached th (the REST threshold
-// score, NaN otherwise): with non-negative values a doc's running sums only
-// grow, so an item whose hit stays 0 holds no doc with a final sum >= th.
-template <int S, int DIAG>
-__device__ __forceinline__ void add_rows(float* acc, const Rows& R, int j0, uint32_t (&ld)[kJ],
-                                         float (&v)[kJ], uint32_t n, float th, uint64_t& hit) {
-  if (DIAG & 1) {  // ablation: consume the loads, no adds
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) asm volatile("" ::"v"(ld[j]), "v"(v[j]));
-    return;
-  }
-  const int nr = rows_done(n);
-  if (nr == kJ)
-    rmw_rows<S, kJ>(acc, R, j0, ld, v, th, hit);
-  else if (nr > 0)
-    rmw_rows<S, kJ / 2>(acc, R, j0, ld, v, th, hit);
-}
-
-// The final sums of an item's processed rows (add_rows' ranges of the D and
-// X blocks, nr rows in all), each read once and cleared; x = 0 elsewhere.
-__device__ __forceinline__ void read_clear(float* acc, const uint32_t (&l0)[kJ],
-                                           const uint32_t (&l1)[kJ], uint32_t nr,
-                                           float (&x)[2 * kJ]) {
-  const uint32_t n0 = min(nr, (uint32_t)kJ), n1 = nr > (uint32_t)kJ ? nr - kJ : 0u;
-  const int r0 = rows_done(n0), r1 = rows_done(n1);
-#pragma unroll
-  for (int j = 0; j < 2 * kJ; ++j) x[j] = 0.f;
-#pragma unroll
-  for (int j = 0; j < kJ; ++j) {
-    if (r0 > 0 && (j < kJ / 2 || r0 == kJ)) {
-      x[j] = acc[l0[j]];
-      acc[l0[j]] = 0.f;
-    }
-  }
-  if (r1 > 0) {
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      if (j < kJ / 2 || r1 == kJ) {
-        x[kJ + j] = acc[l1[j]];
-        acc[l1[j]] = 0.f;
-      }
-    }
-  }
-}
-
-// Clears the processed rows' slots (read_clear without the reads).
-__device__ __forceinline__ void clear_rows(float* acc, const uint32_t (&l0)[kJ],
-                                           const uint32_t (&l1)[kJ], uint32_t nr) {
-  const uint32_t n0 = min(nr, (uint32_t)kJ), n1 = nr > (uint32_t)kJ ? nr - kJ : 0u;
-  const int r0 = rows_done(n0), r1 = rows_done(n1);
-#pragma unroll
-  for (int j = 0; j < kJ; ++j)
-    if (r0 > 0 && (j < kJ / 2 || r0 == kJ)) acc[l0[j]] = 0.f;
-  if (r1 > 0) {
-#pragma unroll
-    for (int j = 0; j < kJ; ++j)
-      if (j < kJ / 2 || r1 == kJ) acc[l1[j]] = 0.f;
-  }
-}
-
-// REST emission from the item's own postings (items of at most 2 kJ rows,
-// whose slots are still in registers): each touched doc's final sum is read
-// once — the first read of a doc clears it, so a doc seen again under a later
-// term reads 0 — and passes iff its key beats theta.  Exact when theta's
-// score is > 0: untouched docs (sum 0) and cleared re-reads can never pass,
-// and every touched doc is read after its last add.  The same reads return
-// the accumulator to all zeros for the next item.  Slots are add_rows'
-// (masked lanes hold their trash slot, which reads 0).
-__device__ __forceinline__ void emit_sparse(float* acc, const uint32_t (&l0)[kJ],
-                                            const uint32_t (&l1)[kJ], uint32_t nr, int64_t tile,
-                                            int S, uint64_t theta, uint64_t* __restrict__ list,
-                                            int32_t* __restrict__ cnt, int32_t C) {
-  const uint32_t lane = lane_id();
-  float x[2 * kJ];
-  read_clear(acc, l0, l1, nr, x);
-  const float th = key_score((uint32_t)(theta >> 32));
-  const int64_t base = tile << S;
-  // ties pass for tile-local docs < tie (clamped to [-1, 2^S])
-  const int tie = (int)max<int64_t>(
-      -1, min<int64_t>(1 << S, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base + 1));
-  uint32_t pm = 0;
-#pragma unroll
-  for (int j = 0; j < 2 * kJ; ++j) {
-    const int l = (int)(j < kJ ? l0[j] : l1[j - kJ]);
-    pm |= (uint32_t)((x[j] > th) | ((x[j] == th) & (l < tie))) << j;
-  }
-  if (__ballot(pm != 0) == 0) return;  // common: nothing of this item passes
-  const int c = __popc(pm);
-  const uint32_t incl = wave_incl_scan((uint32_t)c);
-  int pos = 0;
-  if (lane == 63) pos = atomicAdd(cnt, (int)incl);
-  pos = __shfl(pos, 63, 64) + (int)incl - c;
-#pragma unroll
-  for (int j = 0; j < 2 * kJ; ++j) {
-    if ((pm >> j) & 1u) {
-      const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
-      if (pos < C)
-        list[pos] = ((uint64_t)score_key(x[j]) << 32) |
-                    (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + l));
-      ++pos;
-    }
-  }
-}
-
-// Item distribution of the pipelined kernel.  An XCD's items (one contiguous
-// range of the tile-major item order per XCD) are handed out kClaimCH at a
-// time by kClaimM counters per XCD (counter c serves chunks c, c + kClaimM,
-// ...; each on a 256-B line of its own), so at any moment the XCD's waves work
-// on a window of about (waves x kClaimCH) consecutive items: a few tiles, whose
-// posting segments stay in the XCD's L2 across the queries.  A static stride
-// lets waves drift apart (items differ in cost) until the window spans far more
-// tiles than L2 holds.
-// (kClaimCH, kClaimM, kCtrStride: bm25mi_internal.h)
-
-// SAMPLE keys of an item: the best key of each of M equal doc slices of the
-// tile (M distinct real documents; key 0 for a slice without one).  Any M
-// distinct real documents' keys serve theta (a lower bound of the k-th key),
-// and slice maxima cost one pass instead of M extraction rounds.
-//
-// Sparse form (items of at most 2 kJ rows): the touched docs with a positive
-// sum, read and cleared as in emit_sparse.
-template <int M>
-__device__ __forceinline__ void best_sparse(float* acc, const uint32_t (&l0)[kJ],
-                                            const uint32_t (&l1)[kJ], uint32_t nr, int64_t tile,
-                                            int S, uint32_t idoff, uint64_t* __restrict__ out) {
-  float x[2 * kJ];
-  read_clear(acc, l0, l1, nr, x);
-  const int sh = S - (M == 1 ? 0 : (M == 2 ? 1 : 2));  // slice of tile-local doc l: l >> sh
-  uint32_t bk[M], bd[M];
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    bk[i] = 0;
-    bd[i] = 0xFFFFFFFFu;
-  }
-#pragma unroll
-  for (int j = 0; j < 2 * kJ; ++j) {
-    const uint32_t l = j < kJ ? l0[j] : l1[j - kJ];
-    const uint32_t key = x[j] > 0.f ? score_key(x[j]) : 0u;
-    const uint32_t sl = M == 1 ? 0u : (l >> sh);
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      const bool better = sl == (uint32_t)i && (key > bk[i] || (key == bk[i] && key != 0u && l < bd[i]));
-      bd[i] = better ? l : bd[i];
-      bk[i] = better ? key : bk[i];
-    }
-  }
-  const uint32_t base = (uint32_t)(tile << S) + idoff;  // global doc ids (theta_wave_kernel)
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    const uint32_t wm = wave_max_u32(bk[i]);
-    uint64_t key = 0ull;
-    if (wm != 0) {
-      const uint32_t doc = 0xFFFFFFFFu - wave_max_u32(bk[i] == wm ? 0xFFFFFFFFu - bd[i] : 0u);
-      key = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (base + doc));
-    }
-    if (lane_id() == 0) out[i] = key;
-  }
-}
-
 // Dense form (heavier items): every accumulator of the tile (docs past n_docs
 // excluded), then the accumulators are cleared.  Lane entries are in doc
 // order inside each lane (entry_doc), so a slice is a contiguous run of them.
@@ -933,14 +633,6 @@ __device__ __forceinline__ void best1_pos(float* acc, int64_t tile, uint32_t ido
   zero_acc<S>(acc);
   if (lane == 0) *out = key;
 }
-
-// Item of the pipelined kernel: XCD-relative ordinal rit (end = its chunk's
-// end), phase tile ti = the tib-th tile of a band of bw tiles, query qi, and
-// the tile it scores.
-struct Cursor {
-  int32_t rit, end, ti, qi, tile, tib, bw;
-};
-
 // ---------------------------------------------------------------------------
 // Persistent score kernel: kWaves independent waves per workgroup, each with a
 // private 2^S-float LDS accumulator.  The phase's items are tile-major
@@ -986,801 +678,29 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
                     sg.cand_out + qi * sg.cstride + ti * (PH == kSample ? sg.M : kTileM));
   }
 }
-
-// ---------------------------------------------------------------------------
-// Pipelined persistent score kernel (1 <= T <= 64): same items and the same
-// per-document add order as score_wave_kernel.  Item order: band-major — the
-// phase's tiles are cut into bands of `band` consecutive tiles, and inside a
-// band the items run query by query, each query over the band's tiles — so a
-// claimed chunk is one query over consecutive tiles: its terms' segments of
-// neighbouring tiles share cache lines (a light term has a few postings per
-// tile), and the XCD's waves read the same band of every popular term.
-// (Tile-major order, all queries of a tile back to back, re-fetched each
-// light term's lines from beyond L2 for every tile: 17 GB per config-3 REST
-// launch against 1.9 GB of batch-distinct postings.)  Iteration n issues
-//   (1) the query terms of item n+3,
-//   (2) the (indptr, rel) segment bounds of item n+2,
-//   (3) item n's second block of kJ posting rows and item n+1's first block,
-// and then (4) adding item n's rows (a heavy item's further rows are loaded in
-// place) and selecting / emitting its candidates.
-// ---------------------------------------------------------------------------
-template <int S, int PH, bool QMAP, int DIAG, int SM>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4, 4))) void score_pipe_kernel(
-    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t nq_host,
-    const int32_t* __restrict__ nq_dev, const int32_t* __restrict__ qmap,
-    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, uint64_t* __restrict__ list,
-    int32_t* __restrict__ list_cnt, int32_t C, int32_t* __restrict__ wctr, int32_t claim_ch,
-    int32_t claim_m, int64_t cstride, int32_t G, int32_t band, uint64_t* __restrict__ stamps) {
-  constexpr int D = 1 << S;
-  constexpr int DP = D + 64;  // accumulators + one trash slot per lane (add_rows)
-  __shared__ __attribute__((aligned(16))) float acc_all[kWaves * DP];
-  const int wave = uniform((int)(threadIdx.x >> 6));
-  float* acc = acc_all + wave * DP;
-  // diagnostic build only (DIAG & 32): cycles per loop segment
-  uint64_t seg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = 0;
-#define BM25_STAMP(k)                                                           \
-  if (DIAG & 32) {                                                              \
-    __builtin_amdgcn_sched_barrier(0);                                          \
-    uint64_t t_;                                                                \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                          \
-    seg[k] += t_ - t_last;                                                      \
-    t_last = t_;                                                                \
-  }
-  BM25_STAMP(7);
-  const int32_t nq = QMAP ? *nq_dev : nq_host;
-  const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
-  const int64_t nitems = (int64_t)nt * nq;
-  const int64_t per = (nitems + 7) >> 3;
-  const int grp = (int)(blockIdx.x & 7);
-  const uint32_t lo = (uint32_t)(grp * per);
-  const int32_t ngi = (int32_t)max<int64_t>(0, min<int64_t>(nitems, lo + per) - lo);
-  if (ngi == 0) return;  // wave-uniform; no barriers in this kernel
-  const int32_t cm = (int32_t)((blockIdx.x >> 3) * kWaves + wave) % claim_m;
-  int32_t* ctr = wctr + (grp * kClaimM + cm) * kCtrStride;
-  const int tl = min(lane_id(), T - 1);
-  const PostingRsrc pr = posting_rsrc(a);
-
-  // Claims: lane 0 holds the ordinal of the wave's next chunk on its counter,
-  // claimed one chunk ahead of use.
-  auto claim = [&]() -> int32_t {
-    int32_t v = 0;
-    if (lane_id() == 0) v = atomicAdd(ctr, 1);
-    return v;
-  };
-  int32_t pending = claim();
-  // cursor of the next item after c: the next one of c's chunk, else the
-  // first of the pending chunk; past the end it stays on c's item with
-  // rit = ngi, so every stage keeps loading valid addresses
-  const int32_t nfb = nt / band;  // full bands
-  const uint32_t full_items = (uint32_t)nfb * (uint32_t)band * (uint32_t)nq;
-  auto next = [&](Cursor c) -> Cursor {
-    if (c.rit >= ngi) return c;
-    if (c.rit + 1 < c.end) {
-      ++c.rit;
-      if (++c.tib == c.bw) {  // the query's last tile of the band
-        c.tib = 0;
-        c.ti -= c.bw - 1;
-        if (++c.qi == nq) {  // next band
-          c.qi = 0;
-          c.ti += c.bw;
-          c.bw = min(band, nt - c.ti);
-        }
-      } else {
-        ++c.ti;
-      }
-      c.tile = tile_of32<PH>((uint32_t)c.ti, (uint32_t)P, (uint32_t)G);
-      return c;
-    }
-    const int64_t b = ((int64_t)uniform(pending) * claim_m + cm) * claim_ch;
-    if (b >= ngi) {
-      c.rit = c.end = ngi;
-      return c;
-    }
-    pending = claim();
-    Cursor n;
-    n.rit = (int32_t)b;
-    n.end = (int32_t)min<int64_t>(ngi, b + claim_ch);
-    const uint32_t it = lo + (uint32_t)b;
-    uint32_t bb, r, bw;
-    if (it < full_items) {
-      bb = it / ((uint32_t)band * (uint32_t)nq);
-      r = it - bb * (uint32_t)band * (uint32_t)nq;
-      bw = (uint32_t)band;
-    } else {  // the last, partial band
-      bb = (uint32_t)nfb;
-      r = it - full_items;
-      bw = (uint32_t)(nt - nfb * band);
-    }
-    n.qi = (int32_t)(r / bw);
-    n.tib = (int32_t)(r - (uint32_t)n.qi * bw);
-    n.bw = (int32_t)bw;
-    n.ti = (int32_t)(bb * (uint32_t)band) + n.tib;
-    n.tile = tile_of32<PH>((uint32_t)n.ti, (uint32_t)P, (uint32_t)G);
-    return n;
-  };
-  auto terms_of = [&](const Cursor& c) -> int32_t {
-    const int32_t q = QMAP ? qmap[c.qi] : c.qi;
-    return queries[(int64_t)q * T + tl];
-  };
-
-  Cursor c0;  // a chunk "before" the first one: next() takes the pending claim
-  c0.rit = -1;
-  c0.end = 0;
-  c0.ti = c0.qi = c0.tile = c0.tib = 0;
-  c0.bw = 1;
-  Cursor cD = next(c0);
-  if (cD.rit >= ngi) return;
-  zero_acc<S>(acc);
-  acc[D + lane_id()] = 0.f;
-  Cursor cC = next(cD), cB = next(cC), cA = next(cB);
-  // prologue: item 0's first rows, item 1's bounds, item 2's terms
-  int32_t tmD = terms_of(cD), tmC = terms_of(cC), tmB = terms_of(cB);
-  Desc dC = load_desc(a, tmC, cC.tile);
-  Rows rD = make_rows(load_desc(a, tmD, cD.tile), T, 0);
-  uint32_t ltD[kJ];
-  float vD[kJ];
-  issue_rows<DIAG>(pr, rD, 0, ltD, vD);
-  uint64_t thD = PH == kRest ? theta[cD.qi] : 0ull;
-  int32_t nitem = 0;
-  BM25_STAMP(7);
-
-  while (cD.rit < ngi) {
-    ++nitem;
-    // (1) item n's second row block, (2) terms of item n+3, (3) bounds of
-    // item n+2, (4) item n+1's first rows: all issued before item n's adds
-    const uint32_t nrD = rD.nrows;
-    uint32_t ltX[kJ];
-    float vX[kJ];
-    if (nrD > kJ) issue_rows<DIAG>(pr, rD, kJ, ltX, vX);  // (unconditional: 4.98 vs 4.77 ms)
-    const int32_t tmA = terms_of(cA);
-    const Desc dB = load_desc(a, tmB, cB.tile);
-    BM25_STAMP(0);
-    const Rows rC = make_rows(dC, T, 0);
-    uint32_t ltC[kJ];
-    float vC[kJ];
-    issue_rows<DIAG>(pr, rC, 0, ltC, vC);
-    const uint64_t thC = PH == kRest ? theta[cC.qi] : 0ull;
-    BM25_STAMP(1);
-    // (5) item n: adds in row order, then selection
-    const int64_t tile = cD.tile;
-    // REST over a non-negative index: candidates are flagged while adding
-    const bool flagged = PH == kRest && a.nonneg && (uint32_t)(thD >> 32) > score_key(0.f);
-    const float thf = flagged ? key_score((uint32_t)(thD >> 32)) : __builtin_nanf("");
-    uint64_t hit = 0;
-    add_rows<S, DIAG>(acc, rD, 0, ltD, vD, min(nrD, (uint32_t)kJ), thf, hit);
-    if (nrD > kJ) add_rows<S, DIAG>(acc, rD, kJ, ltX, vX, min(nrD - kJ, (uint32_t)kJ), thf, hit);
-    if (nrD > 2 * kJ) {  // heavy item: the remaining rows, block j + kJ issued before block j's adds
-      const Desc dD = load_desc(a, tmD, tile);
-      Rows t = rD;
-      if ((2 * kJ & 63) == 0) t = make_rows(dD, T, 2 * kJ);
-      uint32_t ltY[kJ];
-      float vY[kJ];
-      issue_rows<DIAG>(pr, t, (2 * kJ) & 63, ltY, vY);
-      for (uint32_t j = 2 * kJ; j < nrD; j += kJ) {
-        const uint32_t jn = j + kJ;
-        Rows tn = t;
-        uint32_t ltZ[kJ];
-        float vZ[kJ];
-        if (jn < nrD) {
-          if ((jn & 63) == 0) tn = make_rows(dD, T, jn);
-          issue_rows<DIAG>(pr, tn, (int)(jn & 63), ltZ, vZ);
-        }
-        add_rows<S, DIAG>(acc, t, (int)(j & 63), ltY, vY, min(nrD - j, (uint32_t)kJ), thf, hit);
-        t = tn;
-#pragma unroll
-        for (int i = 0; i < kJ; ++i) {
-          ltY[i] = ltZ[i];
-          vY[i] = vZ[i];
-        }
-      }
-    }
-    BM25_STAMP(2);
-    BM25_STAMP(3);
-    if (DIAG & 4) {  // ablation: no selection
-      zero_acc<S>(acc);
-    } else if (flagged && hit == 0) {  // no doc of this item reaches theta
-      if (nrD <= 2 * kJ)
-        clear_rows(acc, ltD, ltX, nrD);
-      else
-        zero_acc<S>(acc);
-    } else if (PH == kRest && nrD <= 2 * kJ && (uint32_t)(thD >> 32) > score_key(0.f)) {
-      emit_sparse(acc, ltD, ltX, nrD, tile, S, thD, list + (int64_t)cD.qi * C,
-                  list_cnt + cD.qi, C);
-    } else if (PH == kRest) {
-      emit_rest<S>(acc, tile, a.n_docs, thD, list + (int64_t)cD.qi * C, list_cnt + cD.qi, C);
-    } else if (PH == kSample) {
-      uint64_t* out = cand + (int64_t)cD.qi * cstride + (int64_t)cD.ti * SM;
-      if (nrD <= 2 * kJ)
-        best_sparse<SM>(acc, ltD, ltX, nrD, tile, S, (uint32_t)a.doc_offset, out);
-      else
-        best_dense<S, SM>(acc, tile, a.n_docs, (uint32_t)a.doc_offset, out);
-    } else {
-      select_top_lds<S>(acc, tile, a.n_docs, kTileM,
-                        cand + (int64_t)cD.qi * cstride + (int64_t)cD.ti * kTileM);
-    }
-    BM25_STAMP(4);
-    // rotate the pipeline
-    cD = cC;
-    cC = cB;
-    cB = cA;
-    cA = next(cA);
-    tmD = tmC;
-    tmC = tmB;
-    tmB = tmA;
-    dC = dB;
-    rD = rC;
-    thD = thC;
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      ltD[j] = ltC[j];
-      vD[j] = vC[j];
-    }
-    BM25_STAMP(5);
-  }
-  if ((DIAG & 32) && lane_id() == 0) {
-    uint64_t* o = stamps + ((int64_t)blockIdx.x * kWaves + wave) * 8;
-    seg[6] = (uint64_t)nitem;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = seg[k];
-  }
-#undef BM25_STAMP
-}
-
 // ===========================================================================
-// Band score kernel (queries of 1..8 terms; SAMPLE and REST phases).
+// Flat score kernel (queries of 1..64 terms; SAMPLE, REST and ALL).
+// DESIGN.md §4.
 //
-// An ITEM is (query, band of up to 8 consecutive phase tiles); a wave scores
-// the band's tiles one after another in its private LDS accumulator.
-//   * The segment table (indptr + rel of every (tile, term)) is loaded once
-//     per item, one item ahead: lane i * 8 + t holds term t's segment in
-//     tile i.  (Per-tile items load terms, indptr and a rel pair per tile.)
-//   * Postings move in DOUBLE ROWS: lane l holds postings base + 2l and
-//     base + 2l + 1 (base even) — one b32 load of two u16 slots and one
-//     8-byte load of two f32 scores per 128 postings, half the load
-//     instructions of 64-posting rows.
-//   * Every tile iteration issues the SAME loads: the next tile's first two
-//     blocks of kJ2 double rows (rows past its end read posting 0), so the
-//     compiler's vmcnt waits are exact counts; a load issued under a branch
-//     and still in flight makes every later wait drain it (LLVM merges the
-//     paths pessimistically), which is what exposed the per-tile kernel's
-//     second row block.  The next item's first tile is issued during the
-//     current item's last tile.
-// Per tile the adds follow the query-term order exactly, so every document's
-// fp32 sum has the reference's rounding sequence (bm25_native.py:152, scipy
-// csc_matvec).
-// ===========================================================================
-constexpr int kBandT = 8;    // terms served (T <= kBandT)
-constexpr int kBandW = BM25_BANDW;  // tiles per band item
-#ifndef BM25_BAND_ABL  // dev ablations of the band kernel (timing only, wrong results)
-#define BM25_BAND_ABL 0
-#endif
-#ifndef BM25_HL  // row blocks in flight ahead of the adds in a heavy tile (1 or 2)
-#define BM25_HL 1
-#endif
-#ifndef BM25_KJ2
-#define BM25_KJ2 2
-#endif
-constexpr int kJ2 = BM25_KJ2;  // double rows per streamed block
-#ifndef BM25_NB
-#define BM25_NB 2
-#endif
-constexpr int kNB = BM25_NB;   // blocks of the next tile issued one tile ahead
-
-struct BandDesc {  // lane i * 8 + t: term t's segment bounds in tile i (raw)
-  uint32_t ip, r0, r1;  // indptr[term] (nnz < 2^30 on this path), rel pair
-  uint32_t ok;          // segment present (t < T, i < bw, valid term)
-  uint64_t skey;        // REST: best sample key of tile i, ~0: no skip information
-};
-
-struct BandCur {  // XCD-relative item ordinal, its chunk end, band, query, band width
-  int32_t rit, end, b, q, bw;
-};
-
-struct BandTab {  // an item's segment table (lane i * 8 + t) and its threshold
-  uint32_t sb, sl;  // segment [sb, sb + sl) of the posting arrays (sl = 0: none)
-  uint64_t th;      // REST: theta of the item's query
-};
-
-// Row base of the rows past a table's end (issue_rows2).
-constexpr uint32_t kNoRow = 0u;
-
-// A tile's double rows: lane j of the table describes row j0 + j.
-struct Rows2 {
-  uint32_t base;    // even posting index of the row's first posting pair
-  uint32_t lo, hi;  // the row's term segment [lo, hi): its valid postings
-  uint32_t term;    // query term (T past the end)
-  uint32_t nrows;   // rows of the tile (uniform)
-};
-
-// Segment of term s (lane s < T): [beg, beg + len), cut into double rows from
-// beg & ~1.
-__device__ __forceinline__ Rows2 make_rows2(uint32_t beg, uint32_t len, int T, uint32_t j0) {
-  const uint32_t lane = lane_id();
-  len = (int)lane < T ? len : 0u;
-  const uint32_t nr = len == 0 ? 0u : ((beg & 1u) + len + 127u) >> 7;
-  const uint32_t rincl = scan16(nr);  // T <= 8: lanes >= T hold 0
-  Rows2 r;
-  r.nrows = lane_u32(rincl, T - 1);
-  const uint32_t j = j0 + lane;
-  int pos = 0;
-#pragma unroll
-  for (int step = 8; step >= 1; step >>= 1) {
-    if (step > T) continue;  // uniform
-    const int c = pos + step;
-    const uint32_t x = (uint32_t)__shfl((int)rincl, min(c, T) - 1, 64);
-    if (c <= T && x <= j) pos = c;
-  }
-  const uint32_t st = (uint32_t)__shfl((int)(rincl - nr), pos, 64);
-  const uint32_t b = (uint32_t)__shfl((int)beg, pos, 64);
-  const uint32_t l = (uint32_t)__shfl((int)len, pos, 64);
-  const bool in = j < r.nrows;
-  r.base = in ? (b & ~1u) + 128u * (j - st) : kNoRow;
-  r.lo = in ? b : 1u;
-  r.hi = in ? b + l : 0u;
-  r.term = in ? (uint32_t)pos : (uint32_t)T;
-  return r;
-}
-
-// Loads of double rows [j0, j0 + kJ2) of a table: slot pair + score pair per
-// lane.  Every load is issued (static counts); rows past the table read
-// posting 0 (an L1 hit) and are masked later.  (Loading them through a
-// descriptor of zero records instead — range-checked, no memory access — ran
-// the config-3 score pass slower: 5.12 vs 4.75 ms.)
-__device__ __forceinline__ void issue_rows2(const PostingRsrc& pr, const Rows2& R, int j0,
-                                            uint32_t (&ld)[kJ2], float (&v0)[kJ2],
-                                            float (&v1)[kJ2], bool abl = false) {
-  const uint32_t lane = lane_id();
-#if BM25_BAND_ABL & 1  // dev ablation: no posting loads (slots = the lane's own pair)
-  if (abl) {
-#pragma unroll
-    for (int j = 0; j < kJ2; ++j) {
-      ld[j] = (2u * lane + (uint32_t)j * 128u) | ((2u * lane + 1u + (uint32_t)j * 128u) << 16);
-      v0[j] = 1.f;
-      v1[j] = 1.f;
-    }
-    return;
-  }
-#endif
-#pragma unroll
-  for (int j = 0; j < kJ2; ++j) {
-    const uint32_t base = lane_u32(R.base, j0 + j);
-    ld[j] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)(lane * 4u), (int)(base * 2u), 0);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)(lane * 8u), (int)(base * 4u), 0);
-    v0[j] = __uint_as_float((uint32_t)v[0]);
-    v1[j] = __uint_as_float((uint32_t)v[1]);
-  }
-}
-
-#ifndef BM25_BAND_WAVES
-#define BM25_BAND_WAVES 1
-#endif
-#ifndef BM25_BAND_WPE
-#define BM25_BAND_WPE 5
-#endif
-constexpr int kBandWaves = BM25_BAND_WAVES;  // independent waves per band workgroup
-
-template <int S, int PH, int SM, bool SP>
-__global__ __launch_bounds__(64 * kBandWaves) __attribute__((amdgpu_waves_per_eu(BM25_BAND_WPE, BM25_BAND_WPE))) void score_band_kernel(
-    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t G, int32_t nq,
-    const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int64_t cstride,
-    uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
-    int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
-    const uint64_t* __restrict__ skeys, int64_t sstride) {
-  constexpr int D = 1 << S;
-  constexpr int DP = D + 64;
-  __shared__ __attribute__((aligned(16))) float acc_all[kBandWaves * DP];
-  const int wave = uniform((int)(threadIdx.x >> 6));
-  float* acc = acc_all + wave * DP;
-  const uint32_t lane = lane_id();
-  const uint32_t trash = (uint32_t)D + lane;  // this lane's always-zero slot
-  const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
-  const int32_t nb = (nt + kBandW - 1) / kBandW;
-  const int64_t nitems = (int64_t)nb * nq;
-  const int64_t per = (nitems + 7) >> 3;
-  const int grp = (int)(blockIdx.x & 7);
-  const uint32_t lo = (uint32_t)(grp * per);
-  const int32_t ngi = (int32_t)max<int64_t>(0, min<int64_t>(nitems, lo + per) - lo);
-  if (ngi == 0) return;  // wave-uniform; no barriers in this kernel
-  const int32_t cm = (int32_t)((blockIdx.x >> 3) * kBandWaves + wave) % claim_m;
-  int32_t* ctr = wctr + (grp * kClaimM + cm) * kCtrStride;
-  const PostingRsrc pr = posting_rsrc(a);
-  const uint32_t lt = lane & 7u, li = lane >> 3;  // segment lane: tile li, term lt
-  const int64_t nbp = (a.ntiles + 7) >> 3;          // physical bands (sparse seg rows)
-
-  auto claim = [&]() -> int32_t {
-    int32_t v = 0;
-    if (lane == 0) v = atomicAdd(ctr, 1);
-    return v;
-  };
-  int32_t pending = claim();
-  auto next = [&](BandCur c) -> BandCur {  // as score_pipe_kernel's next(), items = bands
-    if (c.rit >= ngi) return c;
-    if (c.rit + 1 < c.end) {
-      ++c.rit;
-      if (++c.q == nq) {
-        c.q = 0;
-        ++c.b;
-        c.bw = min(kBandW, nt - c.b * kBandW);
-      }
-      return c;
-    }
-    const int64_t bb = ((int64_t)uniform(pending) * claim_m + cm) * claim_ch;
-    if (bb >= ngi) {
-      c.rit = c.end = ngi;
-      return c;
-    }
-    pending = claim();
-    BandCur n;
-    n.rit = (int32_t)bb;
-    n.end = (int32_t)min<int64_t>(ngi, bb + claim_ch);
-    const uint32_t it = lo + (uint32_t)bb;
-    n.b = (int32_t)(it / (uint32_t)nq);
-    n.q = (int32_t)(it - (uint32_t)n.b * (uint32_t)nq);
-    n.bw = min(kBandW, nt - n.b * kBandW);
-    return n;
-  };
-  auto terms_of = [&](const BandCur& c) -> int32_t {
-    return queries[(int64_t)c.q * T + (int)min(lt, (uint32_t)(T - 1))];
-  };
-  // REST: tile li of band b is a sample tile (sample groups of 8 tiles =
-  // bands) iff b % P == 0; its best sample key is skeys[q][(b / P) * 8 + li]
-  const bool skipping = PH == kRest && skeys != nullptr && G == kBandW;
-  auto load_bdesc = [&](const BandCur& c, int32_t tm) -> BandDesc {
-    BandDesc d;
-    const int32_t term = __shfl(tm, (int)lt, 64);
-    const bool ok = (int)lt < T && (int)li < c.bw && term >= 0 && term < a.V;
-    const int64_t tt = ok ? term : 0;
-    const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b * kBandW + li), (uint32_t)P,
-                                                      (uint32_t)G)
-                            : 0;
-    if constexpr (SP) {  // this search's segment table (seg_table_kernel)
-      const uint64_t e =
-          ok ? a.seg[((int64_t)c.q * nbp + (tile >> 3)) * 64 + lt * 8 + (tile & 7)] : 0ull;
-      d.ip = 0u;
-      d.r0 = (uint32_t)e;
-      d.r1 = (uint32_t)e + (uint32_t)(e >> 32);
-    } else {
-      const uint32_t* r = a.rel + tt * (a.ntiles + 1) + tile;
-      d.ip = (uint32_t)a.indptr[tt];
-      d.r0 = r[0];
-      d.r1 = r[1];
-    }
-    d.ok = ok ? 1u : 0u;
-    const int64_t si = (int64_t)(c.b / P) * kBandW + min(li, (uint32_t)(c.bw - 1));
-    d.skey = skipping ? skeys[(int64_t)c.q * sstride + min<int64_t>(si, sstride - 1)] : ~0ull;
-    if (!(skipping && (c.b % P) == 0)) d.skey = ~0ull;
-    return d;
-  };
-  // the item's table; REST: a sample tile whose best key scores below theta
-  // holds no key of the list, so its segments are dropped (exact for m = 1
-  // samples; only when theta is a positive score — no threshold and the
-  // zero-fill case must still see every doc)
-  auto make_tab = [&](const BandDesc& d, uint64_t th) -> BandTab {
-    BandTab tb;
-    const bool th_pos = PH == kRest && (uint32_t)(th >> 32) > score_key(0.f);
-    const bool skip = skipping && th_pos && (uint32_t)(d.skey >> 32) < (uint32_t)(th >> 32);
-    tb.sb = d.ip + d.r0;
-    tb.sl = (d.ok && !skip) ? d.r1 - d.r0 : 0u;
-    tb.th = th;
-    return tb;
-  };
-  auto tile_rows = [&](const BandTab& tb, int i, uint32_t j0) -> Rows2 {
-    const int src = i * 8 + (int)lt;
-    return make_rows2((uint32_t)__shfl((int)tb.sb, src, 64), (uint32_t)__shfl((int)tb.sl, src, 64),
-                      T, j0);
-  };
-
-  BandCur c0;
-  c0.rit = -1;
-  c0.end = 0;
-  c0.b = c0.q = 0;
-  c0.bw = 1;
-  BandCur cur = next(c0);
-  if (cur.rit >= ngi) return;
-  zero_acc<S>(acc);
-  acc[D + lane] = 0.f;
-  // prologue: the first item's table (one exposed load chain), the next
-  // item's descriptors in flight
-  BandTab tab = make_tab(load_bdesc(cur, terms_of(cur)), PH == kRest ? theta[cur.q] : 0ull);
-  BandCur nx = next(cur);
-  BandDesc dN = load_bdesc(nx, terms_of(nx));
-  uint64_t thN = PH == kRest ? theta[nx.q] : 0ull;
-  BandCur nx2 = next(nx);
-  int32_t tmN2 = terms_of(nx2);
-  Rows2 rD = tile_rows(tab, 0, 0);
-  uint32_t ltD[kNB][kJ2];
-  float vD0[kNB][kJ2], vD1[kNB][kJ2];
-#pragma unroll
-  for (int k = 0; k < kNB; ++k) issue_rows2(pr, rD, k * kJ2, ltD[k], vD0[k], vD1[k], PH == kRest);
-  BandCur nx3 = nx2;
-  int32_t tmN3 = tmN2;
-
-  while (cur.rit < ngi) {
-    BandTab ntab = tab;
-    for (int i = 0; i < cur.bw; ++i) {
-      const bool last = i + 1 == cur.bw;
-      const int64_t ti = (int64_t)cur.b * kBandW + i;  // phase tile (SAMPLE: sample index)
-      const int64_t tile = tile_of32<PH>((uint32_t)ti, (uint32_t)P, (uint32_t)G);
-      const uint32_t nrD = rD.nrows;
-      // ---- on the item's last tile: the next item's table (descriptors
-      // loaded one item ago), the descriptors of the one after it and the
-      // terms of the one after that (claims are consumed here, where only
-      // this tile's old row blocks are in flight)
-      if (last) {
-        nx3 = next(nx2);
-        tmN3 = terms_of(nx3);
-        ntab = make_tab(dN, thN);
-        dN = load_bdesc(nx2, tmN2);
-        thN = PH == kRest ? theta[nx2.q] : 0ull;
-      }
-      // ---- the next tile's first kNB blocks (of this item or the next)
-      Rows2 rC = last ? tile_rows(ntab, 0, 0) : tile_rows(tab, i + 1, 0);
-      if (last && nx.rit >= ngi) rC.nrows = 0;
-      uint32_t ltC[kNB][kJ2];
-      float vC0[kNB][kJ2], vC1[kNB][kJ2];
-#pragma unroll
-      for (int k = 0; k < kNB; ++k) issue_rows2(pr, rC, k * kJ2, ltC[k], vC0[k], vC1[k], PH == kRest);
-
-      const uint64_t th = tab.th;
-      const float thf_raw = key_score((uint32_t)(th >> 32));
-      const bool th_pos = PH == kRest && (uint32_t)(th >> 32) > score_key(0.f);
-      // REST over a non-negative index: candidates are flagged while adding
-      const bool flagged = PH == kRest && a.nonneg && th_pos;
-      const float thf = flagged ? thf_raw : __builtin_nanf("");
-      uint64_t hit = 0;
-      // ---- adds in row order (= query-term order: a term's rows are
-      // consecutive); the next row's reads go before this row's writes when
-      // both rows are of one term (distinct docs), after them otherwise
-      auto block = [&](const Rows2& R, int j0, uint32_t (&ld)[kJ2], float (&v0)[kJ2],
-                       float (&v1)[kJ2], uint32_t n) {
-        int tm[kJ2];
-#pragma unroll
-        for (int j = 0; j < kJ2; ++j) {
-          tm[j] = (uint32_t)j < n ? (int)lane_u32(R.term, j0 + j) : -1 - j;
-          const uint32_t p = lane_u32(R.base, j0 + j) + 2u * lane;
-          const uint32_t l0 = lane_u32(R.lo, j0 + j), l1 = lane_u32(R.hi, j0 + j);
-          const bool m0 = p >= l0 && p < l1, m1 = p + 1u >= l0 && p + 1u < l1;
-          ld[j] = (m0 ? (ld[j] & 0xFFFFu) : trash) | ((m1 ? (ld[j] >> 16) : trash) << 16);
-          v0[j] = m0 ? v0[j] : 0.f;
-          v1[j] = m1 ? v1[j] : 0.f;
-        }
-        if (n == 0) return;
-#if BM25_BAND_ABL & 2  // dev ablation: no LDS adds (loads consumed by the hit flags)
-        if (PH == kRest) {
-#pragma unroll
-        for (int j = 0; j < kJ2; ++j)
-          if ((uint32_t)j < n)
-            hit |= __ballot(v0[j] + v1[j] + (float)ld[j] >= 1e30f);
-        return;
-        }
-#endif
-        float x0 = acc[ld[0] & 0xFFFFu], x1 = acc[ld[0] >> 16];
-#pragma unroll
-        for (int j = 0; j < kJ2; ++j) {
-          if ((uint32_t)j < n) {
-            const bool same = j + 1 < kJ2 && tm[j + 1] == tm[j];
-            float n0 = 0.f, n1 = 0.f;
-            if (same) {
-              n0 = acc[ld[j + 1] & 0xFFFFu];
-              n1 = acc[ld[j + 1] >> 16];
-            }
-            const float y0 = x0 + v0[j], y1 = x1 + v1[j];
-            acc[ld[j] & 0xFFFFu] = y0;
-            acc[ld[j] >> 16] = y1;
-            hit |= __ballot(y0 >= thf) | __ballot(y1 >= thf);
-            if (j + 1 < kJ2 && (uint32_t)(j + 1) < n && !same) {
-              n0 = acc[ld[j + 1] & 0xFFFFu];
-              n1 = acc[ld[j + 1] >> 16];
-            }
-            x0 = n0;
-            x1 = n1;
-          }
-        }
-      };
-#pragma unroll
-      for (int k = 0; k < kNB; ++k)
-        block(rD, k * kJ2, ltD[k], vD0[k], vD1[k],
-              nrD > (uint32_t)(k * kJ2) ? min(nrD - k * kJ2, (uint32_t)kJ2) : 0u);
-
-#if BM25_BAND_ABL & 4  // dev ablation: REST emits nothing
-      if (PH == kRest) hit = 0;
-#endif
-      if (nrD > kNB * kJ2) {
-        // ---- a heavy tile: the remaining rows, block j + kJ2 always issued
-        // before block j's adds (past the end: posting 0); dense selection
-        Rows2 t = rD;
-        if (((kNB * kJ2) & 63) == 0) t = tile_rows(tab, i, kNB * kJ2);
-        uint32_t ltY[kJ2];
-        float vY0[kJ2], vY1[kJ2];
-        issue_rows2(pr, t, (kNB * kJ2) & 63, ltY, vY0, vY1, PH == kRest);
-#if BM25_HL == 2
-        // a second block in flight: rows kNB * kJ2 + kJ2 .. (dead past the end)
-        Rows2 tw = t;
-        {
-          const uint32_t jw = kNB * kJ2 + kJ2;
-          if (jw < nrD && (jw & 63) == 0) tw = tile_rows(tab, i, jw);
-          if (jw >= nrD) {
-            tw.base = kNoRow;
-            tw.hi = 0u;
-          }
-        }
-        uint32_t ltW[kJ2];
-        float vW0[kJ2], vW1[kJ2];
-        issue_rows2(pr, tw, (int)((kNB * kJ2 + kJ2) & 63), ltW, vW0, vW1, PH == kRest);
-#endif
-        for (uint32_t j = kNB * kJ2; j < nrD; j += kJ2) {
-          const uint32_t jn = j + BM25_HL * kJ2;
-#if BM25_HL == 2
-          Rows2 tn = tw;
-#else
-          Rows2 tn = t;
-#endif
-          if (jn < nrD && (jn & 63) == 0) tn = tile_rows(tab, i, jn);
-          if (jn >= nrD) {  // nothing left: a dead block keeps the load count static
-            tn.base = kNoRow;
-            tn.hi = 0u;
-          }
-          uint32_t ltZ[kJ2];
-          float vZ0[kJ2], vZ1[kJ2];
-          issue_rows2(pr, tn, (int)(jn & 63), ltZ, vZ0, vZ1, PH == kRest);
-          block(t, (int)(j & 63), ltY, vY0, vY1, min(nrD - j, (uint32_t)kJ2));
-#if BM25_HL == 2
-          t = tw;
-          tw = tn;
-#pragma unroll
-          for (int u = 0; u < kJ2; ++u) {
-            ltY[u] = ltW[u];
-            vY0[u] = vW0[u];
-            vY1[u] = vW1[u];
-            ltW[u] = ltZ[u];
-            vW0[u] = vZ0[u];
-            vW1[u] = vZ1[u];
-          }
-#else
-          t = tn;
-#pragma unroll
-          for (int u = 0; u < kJ2; ++u) {
-            ltY[u] = ltZ[u];
-            vY0[u] = vZ0[u];
-            vY1[u] = vZ1[u];
-          }
-#endif
-        }
-        if (flagged && hit == 0)
-          zero_acc<S>(acc);
-        else if (PH == kRest)
-          emit_rest<S>(acc, tile, a.n_docs, th, list + (int64_t)cur.q * C, list_cnt + cur.q, C);
-        else
-          best_dense<S, SM>(acc, tile, a.n_docs, (uint32_t)a.doc_offset,
-                            cand + (int64_t)cur.q * cstride + ti * SM);
-      } else {
-        // ---- selection / emission from the touched slots (the D blocks'
-        // masked slot pairs); the accumulator is left zeroed
-        auto for_ops = [&](auto&& f) {
-#pragma unroll
-          for (int k = 0; k < kNB; ++k)
-#pragma unroll
-            for (int j = 0; j < kJ2; ++j)
-              if ((uint32_t)(k * kJ2 + j) < nrD) {
-                f(ltD[k][j] & 0xFFFFu);
-                f(ltD[k][j] >> 16);
-              }
-        };
-        auto clear_ops = [&]() { for_ops([&](uint32_t s) { acc[s] = 0.f; }); };
-        if (flagged && hit == 0) {  // no doc of this tile reaches theta
-          clear_ops();
-        } else if (PH == kRest && th_pos && a.nonneg) {
-          // two passes: count (a passing sum is marked by negating it — sums
-          // are >= 0 here — so a doc reached twice counts once), then write
-          // the marked ones in the same order
-          const int64_t base = tile << S;
-          const int tie = (int)max<int64_t>(
-              -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)th) - base + 1));
-          int cnt = 0;
-          for_ops([&](uint32_t s) {
-            const float x = acc[s];
-            const bool pass = (x > thf_raw) | ((x == thf_raw) & ((int)s < tie));
-            if (pass) acc[s] = -x;
-            cnt += pass;
-          });
-          if (__ballot(cnt > 0) != 0) {
-            const uint32_t incl = wave_incl_scan((uint32_t)cnt);
-            int pos = 0;
-            if (lane == 63) pos = atomicAdd(list_cnt + cur.q, (int)incl);
-            pos = __shfl(pos, 63, 64) + (int)incl - cnt;
-            uint64_t* lq = list + (int64_t)cur.q * C;
-            for_ops([&](uint32_t s) {
-              const float x = acc[s];
-              if (x < 0.f) {
-                if (pos < C) lq[pos] = ((uint64_t)score_key(-x) << 32) |
-                                       (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + s));
-                ++pos;
-                acc[s] = 0.f;
-              }
-            });
-          }
-          clear_ops();
-        } else if (PH == kRest) {
-          emit_rest<S>(acc, tile, a.n_docs, th, list + (int64_t)cur.q * C, list_cnt + cur.q, C);
-        } else {  // SAMPLE: the best key of each of SM doc slices of the tile
-          const int sh = S - (SM == 1 ? 0 : (SM == 2 ? 1 : 2));
-          uint32_t bk[SM], bd[SM];
-#pragma unroll
-          for (int u = 0; u < SM; ++u) {
-            bk[u] = 0;
-            bd[u] = 0xFFFFFFFFu;
-          }
-          for_ops([&](uint32_t s) {
-            const float x = acc[s];
-            const uint32_t key = (x > 0.f && s < (uint32_t)D) ? score_key(x) : 0u;
-            const uint32_t sli = SM == 1 ? 0u : (s >> sh);
-#pragma unroll
-            for (int u = 0; u < SM; ++u) {
-              const bool better =
-                  sli == (uint32_t)u && (key > bk[u] || (key == bk[u] && key != 0u && s < bd[u]));
-              bd[u] = better ? s : bd[u];
-              bk[u] = better ? key : bk[u];
-            }
-          });
-          clear_ops();
-          const uint32_t base = (uint32_t)(tile << S) + (uint32_t)a.doc_offset;
-          uint64_t* out = cand + (int64_t)cur.q * cstride + ti * SM;
-#pragma unroll
-          for (int u = 0; u < SM; ++u) {
-            const uint32_t wm = wave_max_u32(bk[u]);
-            uint64_t key = 0ull;
-            if (wm != 0) {
-              const uint32_t doc =
-                  0xFFFFFFFFu - wave_max_u32(bk[u] == wm ? 0xFFFFFFFFu - bd[u] : 0u);
-              key = ((uint64_t)wm << 32) | (uint64_t)(0xFFFFFFFFu - (base + doc));
-            }
-            if (lane == 0) out[u] = key;
-          }
-        }
-      }
-      // ---- rotate
-      rD = rC;
-#pragma unroll
-      for (int k = 0; k < kNB; ++k)
-#pragma unroll
-        for (int j = 0; j < kJ2; ++j) {
-          ltD[k][j] = ltC[k][j];
-          vD0[k][j] = vC0[k][j];
-          vD1[k][j] = vC1[k][j];
-        }
-    }
-    // ---- next item (its first tile is in flight)
-    tab = ntab;
-    cur = nx;
-    nx = nx2;
-    nx2 = nx3;
-    tmN2 = tmN3;
-  }
-}
-
-// ===========================================================================
-// Flat score kernel (queries of 1..8 terms; SAMPLE and REST).  DESIGN.md §4.
-//
-// The band kernel's items — (query, band of up to 8 phase tiles), claimed per
-// XCD — but the wave streams the posting rows of all its items as ONE
-// sequence that ignores tile and item boundaries:
+// Items: (query, band of up to BW consecutive phase tiles), claimed per XCD.
+// An item's 64 lanes describe its (tile, term) posting segments, lane =
+// tile * 2^TL + term: TL = 3 (T <= 8, up to 8 tiles per item), 4 (T <= 16,
+// 4 tiles), 5 (T <= 32, 2 tiles), 6 (T <= 64, 1 tile).  The wave streams the
+// posting rows of all its items as ONE sequence that ignores tile and item
+// boundaries:
 //   * an item's rows (double rows, each inside one (tile, term) segment;
 //     tile-major, query-term order inside a tile) are numbered once per item
-//     by a scan over its 64 (tile, term) segments; a CHUNK of up to 64 rows is
-//     one table, lane r = row r (flat_chunk: a binary search of the scan);
+//     by a scan over its 64 segments; a CHUNK of up to 64 rows is one table,
+//     lane r = row r (flat_chunk: a binary search of the scan);
 //   * a ring of kFR rows is in flight: the step that adds row r issues row
 //     r + kFR into the registers row r freed, so loads never pause at a tile
 //     or item edge and every step issues the same loads (static vmcnt);
-//   * a row of another tile than the accumulator's first runs that tile's
-//     epilogue (REST: the keys >= theta, or a plain clear when no add reached
-//     theta; SAMPLE: the tile's best key per slice).
-// Per tile there is no row-table work, no refill of the pipeline and no
-// per-tile branch structure: the per-item fixed cost of the band kernel
-// (ablation: 2.49 of its 4.35 ms with no loads, adds or emission) is what
-// this removes.  Each doc's adds stay in query-term order (bm25_native.py:152).
+//   * a row of another tile than the accumulator's runs that tile's epilogue
+//     (REST: the keys >= theta, or a plain clear when no add reached theta;
+//     SAMPLE: the tile's best key per slice; ALL: the tile's exact top-4).
+// Each doc's adds stay in query-term order (bm25_native.py:152).
 // ===========================================================================
-#ifndef BM25_FR    // rows in flight (ring slots): REST, SAMPLE
+#ifndef BM25_FR    // rows in flight (ring slots): REST / ALL, SAMPLE
 #define BM25_FR 10
 #endif
 #ifndef BM25_FR_S
@@ -1804,7 +724,11 @@ __device__ __forceinline__ uint32_t scan64(uint32_t x) {
   return x;
 }
 
-struct FlatDesc {   // lane i * 8 + t: term t's segment in tile i (raw; r1 == r0: none)
+struct FlatCur {    // XCD-relative item ordinal, its claim's end, band, stage query, batch row, band width
+  int32_t rit, end, b, q, qb, bw;
+};
+
+struct FlatDesc {   // lane tile * 2^TL + term: the term's segment in the tile (raw; r1 == r0: none)
   uint32_t ip, r0, r1;
   uint32_t sk;      // REST: score-key half of the tile's best sample key (sample tiles)
 };
@@ -1812,7 +736,7 @@ struct FlatDesc {   // lane i * 8 + t: term t's segment in tile i (raw; r1 == r0
 struct FlatTab {    // one chunk of an item's rows: lane r = row j0 + r
   uint32_t base;    // even posting index of the row's first pair (0: dead row)
   uint32_t pk;      // valid postings [lo, hi) of the row's 128 (lo = pk & 1, hi = pk >> 1)
-  uint32_t sid;     // (item serial << 6) | tile * 8 + term; kDeadSid: padding
+  uint32_t sid;     // (item serial << 6) | segment lane; kDeadSid: padding
 };
 
 struct FlatCtx {    // the item a chunk (or the accumulator's tile) belongs to
@@ -1820,7 +744,7 @@ struct FlatCtx {    // the item a chunk (or the accumulator's tile) belongs to
   uint64_t th;
 };
 
-// Rows [j0, j0 + 64) of an item whose (tile, term) lane s holds segment
+// Rows [j0, j0 + 64) of an item whose segment lane s holds segment
 // [sb, sb + sl), rows [excl, incl) of the item.
 __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t incl,
                                               uint32_t excl, uint32_t total, uint32_t j0,
@@ -1848,20 +772,30 @@ __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t
   return t;
 }
 
-template <int S, int PH, int SM, bool SP>
+// Term lanes (log2) of a query width T in 1..64.
+__host__ __device__ inline int flat_tl(int64_t T) {
+  return T <= 8 ? 3 : (T <= 16 ? 4 : (T <= 32 ? 5 : 6));
+}
+
+template <int S, int PH, int SM, bool SP, int TL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WPE, BM25_FLAT_WPE))) void score_flat_kernel(
-    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t G, int32_t nq,
+    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, int32_t P, int32_t G,
+    int32_t nq_host, const int32_t* __restrict__ nq_dev, const int32_t* __restrict__ qmap,
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int64_t cstride,
     uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
     int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
     const uint64_t* __restrict__ skeys, int64_t sstride, int32_t BW) {
   constexpr int D = 1 << S;
   constexpr int kFR = PH == kSample ? BM25_FR_S : BM25_FR;  // ring slots (>= 2)
+  constexpr uint32_t TT = 1u << TL;                          // term lanes per tile
+  constexpr uint32_t kTileMask = (64u >> TL) - 1u;           // tile of a segment lane
   __shared__ __attribute__((aligned(16))) float acc[D + 64];
   const uint32_t lane = lane_id();
   const uint32_t trash = (uint32_t)D + lane;  // this lane's always-zero slot
+  // stage queries: the fallback stage (ALL) reads its count on the device
+  const int32_t nq = (PH == kAll && nq_dev) ? uniform(*nq_dev) : nq_host;
   const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
-  const int32_t nb = (nt + BW - 1) / BW;  // items: (query, BW <= 8 consecutive phase tiles)
+  const int32_t nb = (nt + BW - 1) / BW;  // items: (query, BW consecutive phase tiles)
   const int64_t nitems = (int64_t)nb * nq;
   const int64_t per = (nitems + 7) >> 3;
   const int grp = (int)(blockIdx.x & 7);
@@ -1871,17 +805,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   const int32_t cm = (int32_t)(blockIdx.x >> 3) % claim_m;
   int32_t* ctr = wctr + (grp * kClaimM + cm) * kCtrStride;
   const PostingRsrc pr = posting_rsrc(a);
-  const uint32_t lt = lane & 7u, li = lane >> 3;  // segment lane: tile li, term lt
-  const int64_t nbp = (a.ntiles + 7) >> 3;          // physical bands (sparse seg rows)
+  const uint32_t lt = lane & (TT - 1u), li = lane >> TL;  // segment lane: tile li, term lt
+  const int64_t nbp = (a.ntiles + 7) >> 3;                // 8-tile groups of the sparse seg rows
 
-  // ---- items: claims, terms -> segment descriptors (as score_band_kernel)
+  // ---- items: claims, terms -> segment descriptors
   auto claim = [&]() -> int32_t {
     int32_t v = 0;
     if (lane == 0) v = atomicAdd(ctr, 1);
     return v;
   };
   int32_t pending = claim();
-  auto next = [&](BandCur c) -> BandCur {
+  // batch row of a stage query (ALL: the fallback stage's qmap)
+  auto batch_row = [&](int32_t q) -> int32_t {
+    return (PH == kAll && qmap) ? uniform(qmap[q]) : q;
+  };
+  auto next = [&](FlatCur c) -> FlatCur {
     if (c.rit >= ngi) return c;
     if (c.rit + 1 < c.end) {
       ++c.rit;
@@ -1890,6 +828,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
         ++c.b;
         c.bw = min(BW, nt - c.b * BW);
       }
+      c.qb = batch_row(c.q);
       return c;
     }
     const int64_t bb = ((int64_t)uniform(pending) * claim_m + cm) * claim_ch;
@@ -1898,17 +837,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       return c;
     }
     pending = claim();
-    BandCur n;
+    FlatCur n;
     n.rit = (int32_t)bb;
     n.end = (int32_t)min<int64_t>(ngi, bb + claim_ch);
     const uint32_t it = lo + (uint32_t)bb;
     n.b = (int32_t)(it / (uint32_t)nq);
     n.q = (int32_t)(it - (uint32_t)n.b * (uint32_t)nq);
+    n.qb = batch_row(n.q);
     n.bw = min(BW, nt - n.b * BW);
     return n;
   };
-  auto terms_of = [&](const BandCur& c) -> int32_t {
-    return queries[(int64_t)c.q * T + (int)min(lt, (uint32_t)(T - 1))];
+  auto terms_of = [&](const FlatCur& c) -> int32_t {
+    return queries[(int64_t)c.qb * T + (int)min(lt, (uint32_t)(T - 1))];
   };
   // REST: sample tiles (groups of G = kSampleGroup tiles, one group per G * P)
   // whose best sample key is below theta are skipped
@@ -1917,17 +857,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // an item's segment descriptors (4 VGPRs: a lane outside the item reads its
   // r1 from r0's address, so r1 - r0 = 0 needs no flag; the sample-tile test
   // is redone from the item cursor at enter_item)
-  auto load_bdesc = [&](const BandCur& c, int32_t tm) -> FlatDesc {
+  auto load_bdesc = [&](const FlatCur& c, int32_t tm) -> FlatDesc {
     FlatDesc d;
-    const int32_t term = __shfl(tm, (int)lt, 64);
+    const int32_t term = tm;
     const bool ok = (int)lt < T && (int)li < c.bw && term >= 0 && term < a.V;
     const int64_t tt = ok ? term : 0;
     const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b * BW + li), (uint32_t)P,
                                                       (uint32_t)G)
                             : 0;
     if constexpr (SP) {  // outside the item: the zero entry past the table
-      const uint64_t e = a.seg[ok ? ((int64_t)c.q * nbp + (tile >> 3)) * 64 + lt * 8 + (tile & 7)
-                                  : (int64_t)nq * nbp * 64];
+      const uint64_t e = a.seg[ok ? ((int64_t)c.qb * nbp + (tile >> 3)) * (8 * TT) + lt * 8 + (tile & 7)
+                                  : a.seg_zero];
       d.ip = 0u;
       d.r0 = (uint32_t)e;
       d.r1 = (uint32_t)e + (uint32_t)(e >> 32);
@@ -1952,12 +892,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     return (uint32_t)(th >> 32) > score_key(0.f);
   };
 
-  // ---- the issue side's item: its segments (lane s = tile * 8 + term) and
+  // ---- the issue side's item: its segments (lane s = tile * TT + term) and
   // row numbering; the item prefetch pipeline one and two items ahead
   uint32_t iSb = 0, iSl = 0, iIncl = 0, iExcl = 0;
   uint32_t iTotal = 0, iR = 0, iJ0 = 0, iSer = 0;
   FlatCtx ctxI{0, 0, 0ull};
-  BandCur nx, nx2;
+  FlatCur nx, nx2;
   FlatDesc dN;
   uint64_t thN = 0ull;
   int32_t tmN2 = 0;
@@ -1970,9 +910,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     iSb = dN.ip + dN.r0;
     iSl = skip ? 0u : dN.r1 - dN.r0;
     uint32_t nr = iSl == 0u ? 0u : ((iSb & 1u) + iSl + 127u) >> 7;
-    // no positive threshold: every tile of the band runs its epilogue (one
-    // row, possibly empty, in each tile)
-    if (PH == kRest && !th_pos && lt == 0u && (int)li < nx.bw) nr = max(nr, 1u);
+    // every tile of the item runs its epilogue (one row, possibly empty, in
+    // each tile): ALL, and REST without a positive threshold
+    if ((PH == kAll || (PH == kRest && !th_pos)) && lt == 0u && (int)li < nx.bw)
+      nr = max(nr, 1u);
     iIncl = scan64(nr);
     iExcl = iIncl - nr;
     iTotal = lane_u32(iIncl, 63);
@@ -1985,7 +926,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     ctxI.b = nx.b;
     ctxI.th = thN;
     // prefetch: descriptors of the item after, terms of the one after that
-    BandCur nx3 = next(nx2);
+    FlatCur nx3 = next(nx2);
     dN = load_bdesc(nx2, tmN2);
     thN = PH == kRest ? theta[nx2.q] : 0ull;
     tmN2 = terms_of(nx3);
@@ -1993,10 +934,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     nx2 = nx3;
   };
 
-  BandCur c0;
+  FlatCur c0;
   c0.rit = -1;
   c0.end = 0;
-  c0.b = c0.q = 0;
+  c0.b = c0.q = c0.qb = 0;
   c0.bw = 1;
   nx = next(c0);
   if (nx.rit >= ngi) return;
@@ -2065,7 +1006,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   bool done = false;
 
   auto epilogue = [&]() {
-    const int32_t ti = ctxE.b * BW + (int32_t)(curTag & 7u);
+    const int32_t ti = ctxE.b * BW + (int32_t)(curTag & kTileMask);
     const int64_t tile = tile_of32<PH>((uint32_t)ti, (uint32_t)P, (uint32_t)G);
     if constexpr (PH == kRest) {
       const bool flagged = a.nonneg && th_positive(ctxE.th);
@@ -2074,6 +1015,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       else
         emit_rest<S>(acc, tile, a.n_docs, ctxE.th, list + (int64_t)ctxE.q * C,
                      list_cnt + ctxE.q, C);
+    } else if constexpr (PH == kAll) {
+      select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + (int64_t)ctxE.q * cstride + tile * kTileM);
     } else {
       uint64_t* out = cand + (int64_t)ctxE.q * cstride + (int64_t)ti * SM;
       if constexpr (SM == 1)
@@ -2106,7 +1049,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   auto step = [&](int s) {
     issue(s);
     if (sidC != kDeadSid) {
-      const uint32_t tag = sidC >> 3;
+      const uint32_t tag = sidC >> TL;
       if (tag != curTag) {
         if (curTag != kNoTag) epilogue();
         hit = 0;
@@ -2738,16 +1681,7 @@ __global__ __launch_bounds__(256) void merge_sorted_kernel(
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-#ifdef BM25_S12
-#define BM25_CASE12(call) case 12: call(12); break;
-#else
-#define BM25_CASE12(call)
-#endif
-#ifdef BM25_S12  // dev: 4096-doc tiles (timing experiments)
-bool tile_shift_supported(int s) { return s == 10 || s == 11 || s == 12; }
-#else
-bool tile_shift_supported(int s) { return s == 10 || s == 11; }
-#endif
+bool tile_shift_supported(int s) { return s == kDefaultTileShift; }
 
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int32_t* d_err,
                                hipStream_t stream) {
@@ -2778,16 +1712,14 @@ hipError_t launch_fill_tiles(const DevIndex& ix, const int32_t* d_indices, hipSt
 }
 
 // Sampling geometry: 1 tile in P is a sample tile reporting m keys (the best
-// of each of m doc slices); the first (P, m) in the order P = BM25_SAMPLE_P
-// (default 8), 4, 2 (powers of two), m = 1, 2, 4 whose sample — over the W
-// doc shards searched together (global threshold) — yields >= 2k keys.
-// Sample tiles come in groups of G = 8 consecutive tiles once the index has
-// at least four such groups (G = 1, every P-th tile, below).  P = 1: no
-// threshold — the exact top-4 path over every tile (small indices).  S =
-// keys per query per shard.
-SampleGeom sample_geom(int64_t ntiles, int k, int W) {
-  const char* e = getenv("BM25_SAMPLE_P");
-  const int pmax = e ? atoi(e) : 8;
+// of each of m doc slices); the first (P, m) in the order P = pmax (the
+// handle's sample_p option, default 8), pmax / 2, ... 2 (powers of two), m =
+// 1, 2, 4 whose sample — over the W doc shards searched together (global
+// threshold) — yields >= 2k keys.  Sample tiles come in groups of G = 8
+// consecutive tiles once the index has at least four such groups (G = 1,
+// every P-th tile, below).  P = 1: no threshold — the exact top-4 path over
+// every tile (small indices).  S = keys per query per shard.
+SampleGeom sample_geom(int64_t ntiles, int k, int W, int pmax) {
   for (int P = 64; P >= 2; P >>= 1) {
     if (P > pmax || ntiles < 2 * P) continue;
     const int G = ntiles >= 4 * kSampleGroup * P ? kSampleGroup : 1;
@@ -2800,8 +1732,8 @@ SampleGeom sample_geom(int64_t ntiles, int k, int W) {
 
 // Every resident workgroup slot of the current device (a multiple of 8, one
 // per XCD round), cached per (kernel, device).
-template <int S, int PH, class K>
-static int persistent_grid(K kernel, int block = 64 * kWaves) {
+template <class K>
+static int persistent_grid(K kernel, int block) {
   static std::mutex mu;
   static std::map<std::pair<const void*, int>, int> cache;
   int dev = 0;
@@ -2813,179 +1745,106 @@ static int persistent_grid(K kernel, int block = 64 * kWaves) {
   int cus = 0, occ = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, 0);
-  const char* e = getenv("BM25_WG_PER_CU");
-  if (e) occ = atoi(e);
   const int g = ((cus * (occ > 0 ? occ : 1) + 7) / 8) * 8;
   cache[key] = g;
   return g;
 }
 
-// The pipelined kernel serves queries of 1..64 terms (BM25_NO_PIPE=1 forces
-// the plain one, which also serves longer queries).
-static bool use_pipe(const DevIndex& ix, int64_t T) {
-  static const bool off = getenv("BM25_NO_PIPE") != nullptr;
-  return !off && T >= 1 && T <= kGroup && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
+// The flat kernel serves queries of 1..64 terms over posting arrays that a
+// buffer resource addresses (32-bit byte offsets: < 2^30 postings) and item
+// ordinals of 32 bits; everything else — and every phase when the handle's
+// `flat` option is 0 — takes score_wave_kernel.
+static bool use_flat(const DevIndex& ix, int64_t T, int64_t Q) {
+  return ix.opt.flat && T >= 1 && T <= 64 && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll &&
+         ix.ntiles * Q < 0x7FFFFFFFll;
 }
 
-// Tiles per band of the item order (BM25_BAND overrides, for tuning).
-static int32_t band_tiles() {
-  const char* e = getenv("BM25_BAND");
-  const int v = e ? atoi(e) : kBand;
-  return v >= 1 && v <= 4096 ? v : kBand;
-}
-
-// Item-claim geometry (BM25_CLAIM_CH / BM25_CLAIM_M override, for tuning).
-static int32_t claim_ch() {
-  const char* e = getenv("BM25_CLAIM_CH");
-  const int v = e ? atoi(e) : kClaimCH;
-  return v >= 1 && v <= 4096 ? v : kClaimCH;
-}
-static int32_t claim_m() {
-  const char* e = getenv("BM25_CLAIM_M");
-  const int v = e ? atoi(e) : 4;
-  return v >= 1 && v <= kClaimM ? v : 4;
-}
-
-// Diagnostic builds (BM25_ABLATE, dev only): 1 = no adds, 4 = no selection,
-// 5 = neither, 32 = s_memtime segment stamps of the REST kernel, printed to
-// stderr per launch.
-template <int S, int PH, bool QMAP, int DIAG, int SM = 1>
-static void launch_pipe(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
-                        const Workspace& ws, hipStream_t st) {
-  if constexpr (PH == kSample && SM == 1) {  // m keys per sample tile: a build per m
-    if (sg.M == 2) {
-      launch_pipe<S, PH, QMAP, DIAG, 2>(ix, q, T, sg, ws, st);
-      return;
-    }
-    if (sg.M == kTileM) {
-      launch_pipe<S, PH, QMAP, DIAG, kTileM>(ix, q, T, sg, ws, st);
-      return;
-    }
-  }
-  const int grid = persistent_grid<S, PH>(score_pipe_kernel<S, PH, QMAP, DIAG, SM>);
-  int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;
-  if (!sg.ctr_zeroed) hipMemsetAsync(wctr, 0, sizeof(int32_t) * kWctrInts, st);
-  uint64_t* stamps = nullptr;
-  if (DIAG & 32) {
-    static uint64_t* buf = nullptr;
-    if (!buf) hipMalloc(&buf, sizeof(uint64_t) * 8 * grid * kWaves);
-    hipMemsetAsync(buf, 0, sizeof(uint64_t) * 8 * grid * kWaves, st);
-    stamps = buf;
-  }
-  hipLaunchKernelGGL((score_pipe_kernel<S, PH, QMAP, DIAG, SM>), dim3((unsigned)grid),
-                     dim3(64 * kWaves), 0, st, args_of(ix), q, (int32_t)T, sg.P, sg.nq_host,
-                     sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, ws.list, ws.list_cnt, ws.list_cap,
-                     wctr, claim_ch(), claim_m(), sg.cstride, sg.G, band_tiles(), stamps);
-  if ((DIAG & 32) && PH == kRest) {
-    std::vector<uint64_t> h(8 * grid * kWaves);
-    hipStreamSynchronize(st);
-    hipMemcpy(h.data(), stamps, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost);
-    double tot[8] = {0};
-    for (size_t i = 0; i < h.size(); ++i) tot[i % 8] += (double)h[i];
-    double loop = 0;
-    for (int k = 0; k < 6; ++k) loop += tot[k];
-    fprintf(stderr, "stamps: items %.0f, per item:", tot[6]);
-    for (int k = 0; k < 6; ++k) fprintf(stderr, " s%d=%.0f", k, tot[k] / tot[6]);
-    fprintf(stderr, " | loop %.0f (s_memtime ticks per wave)\n", loop / tot[6]);
-  }
-}
-
-// Band items claimed per claim of the band kernel (BM25_BAND_CLAIM overrides).
-static int32_t band_claim() {
-  const char* e = getenv("BM25_BAND_CLAIM");
-  const int v = e ? atoi(e) : 1;
-  return v >= 1 && v <= 64 ? v : 1;
-}
-
-// The band kernel serves SAMPLE and REST for queries of 1..8 terms
-// (BM25_NO_BAND=1 forces the per-tile pipelined kernel).
-static bool use_band(const DevIndex& ix, int64_t T) {
-  static const bool off = getenv("BM25_NO_BAND") != nullptr;
-  return !off && T >= 1 && T <= kBandT && (ix.nnz + kPostingPad) * 4 < 0xFFFFFFF0ll;
-}
-
-// The flat kernel replaces the band kernel's tile loop (BM25_FLAT=0: band).
-static bool use_flat() {
-  static const bool off = getenv("BM25_FLAT") && atoi(getenv("BM25_FLAT")) == 0;
-  return !off;
-}
-
-// Tiles per flat-kernel item: 8, halved while the phase would give the
-// resident waves fewer than BM25_ITEMS_PER_WAVE (8) items each — a small doc
-// shard's SAMPLE pass has ~2 eight-tile items per wave, and the last wave's
-// items set the pass time (BM25_FLAT_BW forces a width).
-static int32_t flat_band(int64_t nt, int64_t nq, int grid) {
-  static const int forced = getenv("BM25_FLAT_BW") ? atoi(getenv("BM25_FLAT_BW")) : 0;
-  if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
-  static const int64_t per = getenv("BM25_ITEMS_PER_WAVE") ? atoi(getenv("BM25_ITEMS_PER_WAVE")) : 8;
-  int32_t bw = 8;
-  while (bw > 1 && ((nt + bw - 1) / bw) * nq < per * (int64_t)grid) bw >>= 1;
+// Tiles per flat-kernel item: the most the term lanes allow (64 / 2^TL),
+// halved while the phase would give the resident waves fewer than
+// `items_per_wave` items each — a small doc shard's SAMPLE pass has ~2
+// eight-tile items per wave, and the last wave's items set the pass time.
+// The fallback stage (a few queries, counted on the device) uses 1-tile items.
+static int32_t flat_band(const SearchOpts& o, int64_t nt, int64_t nq, int grid, int bwmax,
+                         bool fallback) {
+  if (o.flat_bw > 0) return std::min(o.flat_bw, bwmax);
+  if (fallback) return 1;
+  int32_t bw = bwmax;
+  while (bw > 1 && ((nt + bw - 1) / bw) * nq < (int64_t)o.items_per_wave * grid) bw >>= 1;
   return bw;
 }
 
-template <int S, int PH, int SM = 1>
-static void launch_band(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
-                        const Workspace& ws, hipStream_t st) {
-  if constexpr (PH == kSample && SM == 1) {  // m keys per sample tile: a build per m
-    if (sg.M == 2) {
-      launch_band<S, PH, 2>(ix, q, T, sg, ws, st);
-      return;
-    }
-    if (sg.M == kTileM) {
-      launch_band<S, PH, kTileM>(ix, q, T, sg, ws, st);
-      return;
-    }
-  }
+int flat_term_lanes(int64_t T) { return 1 << flat_tl(T); }
+
+template <int S, int PH, int SM, int TL>
+static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t Qb,
+                        const Stage& sg, const Workspace& ws, hipStream_t st) {
   int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;
   if (!sg.ctr_zeroed) hipMemsetAsync(wctr, 0, sizeof(int32_t) * kWctrInts, st);
   // REST skips the sample tiles whose best key is below theta (m = 1 samples
-  // in groups of one band: ws.cand holds this shard's sample keys)
-  const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kBandW;
+  // in groups of 8 tiles: ws.cand holds this shard's sample keys)
+  const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kSampleGroup;
   IndexArgs a = args_of(ix);
   a.seg = ws.seg;
-  if (use_flat()) {
-#define BM25_FLAT_LAUNCH(SPV)                                                                     \
-  {                                                                                               \
-    const int grid = persistent_grid<S, PH>(score_flat_kernel<S, PH, SM, SPV>, 64);               \
-    const int64_t nt = PH == kSample ? sample_count(ix.ntiles, sg.P, sg.G) : ix.ntiles;          \
-    hipLaunchKernelGGL((score_flat_kernel<S, PH, SM, SPV>), dim3((unsigned)grid), dim3(64), 0, st, \
-                       a, q, (int32_t)T, sg.P, sg.G, sg.nq_host, ws.theta, sg.cand_out,           \
-                       sg.cstride, ws.list, ws.list_cnt, ws.list_cap, wctr, band_claim(),         \
-                       claim_m(), skip ? sg.sample_keys : nullptr, sg.sample_stride,              \
-                       flat_band(nt, sg.nq_host, grid));                                          \
-  }
-    if (ix.sparse)
-      BM25_FLAT_LAUNCH(true)
-    else
-      BM25_FLAT_LAUNCH(false)
-#undef BM25_FLAT_LAUNCH
-    return;
-  }
-  if (ix.sparse) {
-    const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM, true>, 64 * kBandWaves);
-    hipLaunchKernelGGL((score_band_kernel<S, PH, SM, true>), dim3((unsigned)grid),
-                       dim3(64 * kBandWaves), 0, st, a, q, (int32_t)T, sg.P, sg.G, sg.nq_host,
-                       ws.theta, sg.cand_out, sg.cstride, ws.list, ws.list_cnt, ws.list_cap,
-                       wctr, band_claim(), claim_m(), skip ? sg.sample_keys : nullptr,
-                       sg.sample_stride);
-    return;
-  }
-  const int grid = persistent_grid<S, PH>(score_band_kernel<S, PH, SM, false>, 64 * kBandWaves);
-  hipLaunchKernelGGL((score_band_kernel<S, PH, SM, false>), dim3((unsigned)grid),
-                     dim3(64 * kBandWaves), 0, st, a, q, (int32_t)T, sg.P, sg.G, sg.nq_host, ws.theta,
-                     sg.cand_out, sg.cstride, ws.list, ws.list_cnt, ws.list_cap, wctr,
-                     band_claim(), claim_m(), skip ? sg.sample_keys : nullptr, sg.sample_stride);
+  a.seg_zero = Qb * ((ix.ntiles + 7) >> 3) * 8 * (1 << TL);
+  const int64_t nt = PH == kSample ? sample_count(ix.ntiles, sg.P, sg.G) : ix.ntiles;
+  auto go = [&](auto kern) {
+    const int grid = persistent_grid(kern, 64);
+    const int bw = flat_band(ix.opt, nt, sg.nq_host, grid, 64 >> TL, sg.nq_dev != nullptr);
+    ix.disp.kernels |= PH == kSample ? kKFlatSample : (PH == kRest ? kKFlatRest : kKFlatAll);
+    ix.disp.term_lanes = 1 << TL;
+    ix.disp.band_tiles[PH] = bw;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, st, a, q, (int32_t)T, sg.P,
+                       sg.G, sg.nq_host, sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, sg.cstride,
+                       ws.list, ws.list_cnt, ws.list_cap, wctr, ix.opt.claim_ch, ix.opt.claim_m,
+                       skip ? sg.sample_keys : nullptr, sg.sample_stride, bw);
+  };
+  if (ix.sparse)
+    go(score_flat_kernel<S, PH, SM, true, TL>);
+  else
+    go(score_flat_kernel<S, PH, SM, false, TL>);
 }
 
-// Sparse index, band kernel: the segment of every (band item lane = tile li,
-// query term lt) of the batch, from the query terms' tile lists — one wave
-// per (query, term position) walks its term's non-empty tiles (coalesced
-// reads) and writes (start | len << 32) into seg[q][tile / 8][pos][tile % 8]
-// (a term's entries of one band are one 64-B run); seg was zeroed (empty
-// segments).
+template <int S, int PH, int SM>
+static void launch_flat_tl(const DevIndex& ix, const int32_t* q, int64_t T, int64_t Qb,
+                           const Stage& sg, const Workspace& ws, hipStream_t st) {
+  switch (flat_tl(T)) {
+    case 3: launch_flat<S, PH, SM, 3>(ix, q, T, Qb, sg, ws, st); break;
+    case 4: launch_flat<S, PH, SM, 4>(ix, q, T, Qb, sg, ws, st); break;
+    case 5: launch_flat<S, PH, SM, 5>(ix, q, T, Qb, sg, ws, st); break;
+    default: launch_flat<S, PH, SM, 6>(ix, q, T, Qb, sg, ws, st); break;
+  }
+}
+
+// One score phase of a search over the batch of Qb queries (the stage may
+// cover a subset: the fallback stage's qmap).
+template <int S, int PH>
+static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t T, int64_t Qb,
+                         const Stage& sg, const Workspace& ws, hipStream_t st) {
+  if (use_flat(ix, T, Qb)) {
+    if constexpr (PH == kSample) {  // m keys per sample tile: a build per m
+      if (sg.M == 2) return launch_flat_tl<S, PH, 2>(ix, q, T, Qb, sg, ws, st);
+      if (sg.M == kTileM) return launch_flat_tl<S, PH, kTileM>(ix, q, T, Qb, sg, ws, st);
+    }
+    return launch_flat_tl<S, PH, 1>(ix, q, T, Qb, sg, ws, st);
+  }
+  int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;
+  (void)wctr;
+  ix.disp.kernels |= PH == kSample ? kKWaveSample : (PH == kRest ? kKWaveRest : kKWaveAll);
+  const int grid = persistent_grid(score_wave_kernel<S, PH>, 64 * kWaves);
+  hipLaunchKernelGGL((score_wave_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0, st,
+                     args_of(ix), q, (int32_t)T, sg, ws.theta, sg.cand_out, ws.list, ws.list_cnt,
+                     ws.list_cap);
+}
+
+// Sparse index: the segment of every (query, term position, tile) the flat
+// kernel reads, from the query terms' tile lists — one wave per (query, term
+// position) walks its term's non-empty tiles (coalesced reads) and writes
+// (start | len << 32) into seg[q][tile / 8][pos][tile % 8] (TT term slots per
+// 8-tile group: a term's entries of one group are one 64-B run); seg was
+// zeroed (empty segments).
 __global__ __launch_bounds__(256) void seg_table_kernel(IndexArgs a,
                                                         const int32_t* __restrict__ queries,
-                                                        int64_t Q, int32_t T,
+                                                        int64_t Q, int32_t T, int32_t TT,
                                                         uint64_t* __restrict__ seg) {
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= Q * T) return;  // wave-uniform; no barriers
@@ -2997,12 +1856,12 @@ __global__ __launch_bounds__(256) void seg_table_kernel(IndexArgs a,
   const int64_t b = a.tl_ptr[term], e = a.tl_ptr[term + 1];
   const int64_t ip = a.indptr[term];
   const uint32_t df = (uint32_t)(a.indptr[term + 1] - ip);
-  uint64_t* row = seg + q * nbp * 64;
+  uint64_t* row = seg + q * nbp * 8 * TT;
   for (int64_t i = b + lane_id(); i < e; i += 64) {
     const uint32_t tile = a.tl_tile[i];
     const uint32_t st = a.tl_start[i];
     const uint32_t nx = i + 1 < e ? a.tl_start[i + 1] : df;
-    row[(int64_t)(tile >> 3) * 64 + pos * 8 + (tile & 7)] =
+    row[(int64_t)(tile >> 3) * 8 * TT + pos * 8 + (tile & 7)] =
         (uint64_t)(uint32_t)(ip + st) | ((uint64_t)(nx - st) << 32);
   }
 }
@@ -3029,49 +1888,18 @@ hipError_t launch_max_token(const int32_t* d_queries, int64_t n, int32_t* d_out,
   return hipGetLastError();
 }
 
-int64_t seg_entries(const DevIndex& ix, int64_t Q) {  // + 64 zero entries past the table
-  return ix.sparse ? Q * ((ix.ntiles + 7) >> 3) * 64 + 64 : 0;
+// u64 entries of the per-search segment table (+ 64 zero entries past it).
+int64_t seg_entries(const DevIndex& ix, int64_t Q, int64_t T) {
+  if (!ix.sparse || !use_flat(ix, T, Q)) return 0;
+  return Q * ((ix.ntiles + 7) >> 3) * 8 * flat_term_lanes(T) + 64;
 }
 
 static void launch_seg_table(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
                              const Workspace& ws, hipStream_t st) {
-  hipMemsetAsync(ws.seg, 0, sizeof(uint64_t) * seg_entries(ix, Q), st);
+  hipMemsetAsync(ws.seg, 0, sizeof(uint64_t) * seg_entries(ix, Q, T), st);
   const int64_t waves = Q * T;
   hipLaunchKernelGGL(seg_table_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
-                     args_of(ix), q, Q, (int32_t)T, ws.seg);
-}
-
-template <int S, int PH>
-static void launch_wave(const DevIndex& ix, const int32_t* q, int64_t T, const Stage& sg,
-                        const Workspace& ws, hipStream_t st) {
-  if constexpr (PH != kAll) {
-    if (!sg.qmap && use_band(ix, T) &&
-        ((ix.ntiles + kBandW - 1) / kBandW) * (int64_t)sg.nq_host < 0x7FFFFFFFll) {
-      launch_band<S, PH>(ix, q, T, sg, ws, st);
-      return;
-    }
-  }
-  if (use_pipe(ix, T) && ix.ntiles * (int64_t)sg.nq_host < 0x7FFFFFFFll) {
-    static const int diag = getenv("BM25_ABLATE") ? atoi(getenv("BM25_ABLATE")) : 0;
-    if (sg.qmap)
-      launch_pipe<S, PH, true, 0>(ix, q, T, sg, ws, st);
-    else if (diag == 0)
-      launch_pipe<S, PH, false, 0>(ix, q, T, sg, ws, st);
-    else if (diag == 1)
-      launch_pipe<S, PH, false, 1>(ix, q, T, sg, ws, st);
-    else if (diag == 4)
-      launch_pipe<S, PH, false, 4>(ix, q, T, sg, ws, st);
-    else if (diag == 5)
-      launch_pipe<S, PH, false, 5>(ix, q, T, sg, ws, st);
-
-    else
-      launch_pipe<S, PH, false, 32>(ix, q, T, sg, ws, st);
-    return;
-  }
-  const int grid = persistent_grid<S, PH>(score_wave_kernel<S, PH>);
-  hipLaunchKernelGGL((score_wave_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0, st,
-                     args_of(ix), q, (int32_t)T, sg, ws.theta, sg.cand_out, ws.list, ws.list_cnt,
-                     ws.list_cap);
+                     args_of(ix), q, Q, (int32_t)T, (int32_t)flat_term_lanes(T), ws.seg);
 }
 
 // P > 1: the sampled search (its merge reads the list only: nt = 0);
@@ -3131,7 +1959,7 @@ static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   // counters and the list counts (each was a memset launch: ~5 us apiece)
   hipLaunchKernelGGL(zero_search_kernel, dim3(64), dim3(256), 0, st, keys, Q * g.S, ws.wctr,
                      (int64_t)kWctrRegions * kWctrInts, ws.counters, ws.list_cnt, Q);
-  if (ix.sparse && use_band(ix, T)) launch_seg_table(ix, q, Q, T, ws, st);  // SAMPLE + REST
+  if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, q, Q, T, ws, st);  // SAMPLE + REST + fallback
   Stage sg = main_stage(ix, Q, g.P, ws);
   sg.ctr_region = 0;
   sg.ctr_zeroed = true;
@@ -3139,7 +1967,7 @@ static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   sg.G = g.G;
   sg.cand_out = keys;
   sg.cstride = g.S;
-  launch_wave<S_, kSample>(ix, q, T, sg, ws, st);
+  launch_phase<S_, kSample>(ix, q, T, Q, sg, ws, st);
   if (keys != ws.cand)
     hipMemcpyAsync(ws.cand, keys, sizeof(uint64_t) * Q * g.S, hipMemcpyDeviceToDevice, st);
 }
@@ -3151,11 +1979,12 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
                      const SampleGeom& g, int W, const uint64_t* all_keys, const Workspace& ws,
                      hipStream_t st) {
   Stage sg = main_stage(ix, Q, g.P, ws);
-  if (g.P == 1) {  // no sample pass ran: nothing was zeroed
+  if (g.P == 1) {  // no sample pass ran: nothing was zeroed, no segment table built
     hipMemsetAsync(ws.counters, 0, 4 * sizeof(int32_t), st);
+    if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, q, Q, T, ws, st);
     sg.ctr_region = 2;
     sg.ctr_zeroed = false;
-    launch_wave<S_, kAll>(ix, q, T, sg, ws, st);
+    launch_phase<S_, kAll>(ix, q, T, Q, sg, ws, st);
     return;
   }
   sg.ctr_region = 1;  // counters, list counts and claim counters: zeroed by sample_s
@@ -3167,18 +1996,12 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, st, all_keys,
                      (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap,
                      ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs);
-  launch_wave<S_, kRest>(ix, q, T, sg, ws, st);
+  launch_phase<S_, kRest>(ix, q, T, Q, sg, ws, st);
 }
-
-template <int S_>
-static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k, int P,
-                     const Workspace& ws, int32_t* docs, float* scores, hipStream_t st);
 
 #define BM25_SHIFT_DISPATCH(call)                        \
   switch (ix.tile_shift) {                               \
-    case 10: call(10); break;                            \
-    case 11: call(11); break;                            \
-    BM25_CASE12(call)                                    \
+    case kDefaultTileShift: call(kDefaultTileShift); break; \
     default: return hipErrorInvalidValue;                \
   }
 
@@ -3208,7 +2031,7 @@ hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q
 
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                         int k, const Workspace& ws, hipStream_t stream) {
-  const SampleGeom g = sample_geom(ix.ntiles, k, 1);
+  const SampleGeom g = sample_geom(ix.ntiles, k, 1, ix.opt.sample_p);
   hipError_t e = launch_sample(ix, d_queries, Q, T, g, ws.cand, ws, stream);
   if (e != hipSuccess) return e;
   return launch_finish(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream);
@@ -3239,7 +2062,7 @@ static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   Stage fb = fallback_stage(ix, Q, ws);
   fb.ctr_region = 2;  // unused by the sampled search: zeroed by sample_s
   fb.ctr_zeroed = true;
-  launch_wave<S_, kAll>(ix, q, T, fb, ws, st);
+  launch_phase<S_, kAll>(ix, q, T, Q, fb, ws, st);
   select_stage<S_>(ix, q, T, k, fb, ws, docs, scores, st);
 }
 
@@ -3261,15 +2084,9 @@ hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries, int64_t Q
 hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query, int64_t T,
                                float* d_out, hipStream_t stream) {
   if (ix.ntiles == 0) return hipSuccess;
-  const dim3 grid((unsigned)ix.ntiles);
-  switch (ix.tile_shift) {
-    case 10: hipLaunchKernelGGL(scores_dense_kernel<10>, grid, dim3(64), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
-#ifdef BM25_S12
-    case 12: hipLaunchKernelGGL(scores_dense_kernel<12>, grid, dim3(64), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
-#endif
-    case 11: hipLaunchKernelGGL(scores_dense_kernel<11>, grid, dim3(64), 0, stream, args_of(ix), d_query, (int32_t)T, d_out); break;
-    default: return hipErrorInvalidValue;
-  }
+  if (ix.tile_shift != kDefaultTileShift) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scores_dense_kernel<kDefaultTileShift>, dim3((unsigned)ix.ntiles), dim3(64),
+                     0, stream, args_of(ix), d_query, (int32_t)T, d_out);
   return hipGetLastError();
 }
 

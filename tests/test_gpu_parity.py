@@ -18,19 +18,34 @@ def _load(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 
 
-def _idx(indptr, indices, data, n_docs, shift=None, doc_offset=0):
+def _idx(indptr, indices, data, n_docs, doc_offset=0, segments=None, options=None):
+    """A GpuIndex; ``segments`` = "dense" / "sparse" forces the segment table
+    (BM25_SEGMENTS, read at create), ``options`` are bm25_index_set_option's."""
     from bm25mi.index import GpuIndex
-    old = os.environ.get("BM25_TILE_SHIFT")
-    if shift is not None:
-        os.environ["BM25_TILE_SHIFT"] = str(shift)
+    old = os.environ.get("BM25_SEGMENTS")
+    if segments is not None:
+        os.environ["BM25_SEGMENTS"] = segments
     try:
-        return GpuIndex(indptr, indices, data, n_docs, doc_offset=doc_offset)
+        return GpuIndex(indptr, indices, data, n_docs, doc_offset=doc_offset, options=options)
     finally:
-        if shift is not None:
+        if segments is not None:
             if old is None:
-                os.environ.pop("BM25_TILE_SHIFT")
+                os.environ.pop("BM25_SEGMENTS")
             else:
-                os.environ["BM25_TILE_SHIFT"] = old
+                os.environ["BM25_SEGMENTS"] = old
+
+
+# what a search launches: SAMPLE + REST (+ the fallback stage's ALL launch,
+# which reads its query count on the device), or one exact ALL pass
+FLAT_SAMPLED = {"flat_sample", "flat_rest", "flat_all"}
+WAVE_SAMPLED = {"wave_sample", "wave_rest", "wave_all"}
+
+
+def _progress(msg):
+    """A line per stage of the long full-workload tests (run with -s, so a
+    GPU run shows progress)."""
+    import time
+    print(f"  [{time.strftime('%H:%M:%S')}] {msg}", flush=True)
 
 
 def _exact(a, b):
@@ -130,15 +145,16 @@ def test_dense_scores_bit_exact(gpu):
 
 
 # ------------------------------------------------------- synthetic parity
-@pytest.mark.parametrize("shift", [10, 11])
-def test_tile_shifts_random(gpu, shift):
-    rng = np.random.default_rng(shift)
-    N, V = 70_001, 700
+@pytest.mark.parametrize("seed", [10, 11])
+def test_random_ragged_index(gpu, seed):
+    rng = np.random.default_rng(seed)
+    N, V = 70_001, 700  # a partial last tile
     ip, ix, dt = _rand_index(rng, N, V, 6000)
     q = rng.integers(-1, V, size=(37, 9)).astype(np.int32)
-    index = _idx(ip, ix, dt, N, shift=shift)
+    index = _idx(ip, ix, dt, N)
     for k in (1, 4, 5, 64, 300):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+    assert index.last_dispatch()["term_lanes"] == 16  # T = 9: 16 term lanes, 4 tiles per item
 
 
 def test_signed_and_tied_values(gpu):
@@ -161,14 +177,55 @@ def test_zero_fill_and_k_equals_n(gpu):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
 
 
-def test_long_queries_multiple_term_groups(gpu):
-    rng = np.random.default_rng(4)
-    N, V = 30_000, 400
-    ip, ix, dt = _rand_index(rng, N, V, 3000)
-    q = rng.integers(-1, V, size=(9, 45)).astype(np.int32)
-    q[0, :] = 7  # one term 45 times
+@pytest.mark.parametrize("T,lanes", [(1, 8), (12, 16), (16, 16), (17, 32), (32, 32), (45, 64),
+                                     (64, 64)])
+@pytest.mark.parametrize("segments", ["dense", "sparse"])
+def test_flat_kernel_query_widths(gpu, T, lanes, segments):
+    """Queries of 1..64 terms take the flat kernel with 8/16/32/64 term lanes
+    per tile (64 / lanes tiles per item), on both segment tables: padding,
+    a term repeated across the whole row, duplicates — bit-exact."""
+    rng = np.random.default_rng(T)
+    N, V = 120_000, 500
+    ip, ix, dt = _rand_index(rng, N, V, 12_000)
+    q = rng.integers(-1, V, size=(33, T)).astype(np.int32)
+    q[0, :] = 7          # one term T times
+    q[1, :] = -1         # all padding
+    q[2, T // 2:] = -1
+    index = _idx(ip, ix, dt, N, segments=segments)
+    assert index.info()["sparse"] == (segments == "sparse")
+    for k in (1, 25, 300):
+        _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+        d = index.last_dispatch()
+        sampled = _sample_p(index.info()["n_tiles"], k) > 1
+        assert d["kernels"] == (FLAT_SAMPLED if sampled else {"flat_all"}), d
+        assert d["term_lanes"] == lanes, d
+        assert 1 <= d["band_tiles"]["rest" if sampled else "all"] <= 64 // lanes
+
+
+@pytest.mark.parametrize("T", [0, 65, 80])
+def test_wave_kernel_long_and_empty_queries(gpu, T):
+    """Queries of 0 or more than 64 terms take score_wave_kernel (LDS float
+    adds in query-term order) for SAMPLE, REST and ALL — bit-exact."""
+    rng = np.random.default_rng(80 + T)
+    N, V = 60_000, 400
+    ip, ix, dt = _rand_index(rng, N, V, 6000)
+    q = rng.integers(-1, V, size=(11, T)).astype(np.int32)
+    if T:
+        q[0, :] = 3
+        q[1, :40] = -1
     index = _idx(ip, ix, dt, N)
-    _exact(index.search(q, 25), oracle.search_c(N, ip, ix, dt, q, 25))
+    for k in (1, 30, 200):
+        _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+        sampled = _sample_p(index.info()["n_tiles"], k) > 1
+        assert index.last_dispatch()["kernels"] == (WAVE_SAMPLED if sampled else {"wave_all"})
+    index.set_option("sample_p", 1)  # the exact pass over every tile
+    _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
+    assert index.last_dispatch()["kernels"] == {"wave_all"}
+    index.set_option("list_cap", 4)  # every query through the fallback stage
+    index.set_option("sample_p", 8)
+    _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
+    if T:
+        assert index.search_stats()["fallback_queries"] > 0
 
 
 def test_tiny_and_empty_shapes(gpu):
@@ -184,10 +241,9 @@ def test_tiny_and_empty_shapes(gpu):
     assert one.search(np.array([[0]], np.int32), 1)[0].tolist() == [[0]]
 
 
-def test_rescore_path_clustered_tile(gpu, monkeypatch):
+def test_rescore_path_clustered_tile(gpu):
     # every high score sits in tiles 0-2, so the exact path (no sampling) must
     # rescore them
-    monkeypatch.setenv("BM25_SAMPLE_P", "1")
     N, V = 200_000, 3
     ip = np.array([0, 5000, 5000 + N // 2, 5000 + N // 2 + 10], np.int64)
     ix = np.concatenate([np.arange(5000, dtype=np.int32),
@@ -196,13 +252,15 @@ def test_rescore_path_clustered_tile(gpu, monkeypatch):
     rng = np.random.default_rng(8)
     dt = np.concatenate([rng.uniform(10, 20, 5000), rng.uniform(0, 1, N // 2),
                          rng.uniform(0, 30, 10)]).astype(np.float32)
-    index = _idx(ip, ix, dt, N)
     q = np.array([[0, 1, 2], [1, 0, -1], [2, 2, 1]], np.int32)
-    index.profile_enable(True)
-    for k in (100, 2048):
-        got = index.search(q, k)
-        _exact(got, oracle.search_c(N, ip, ix, dt, q, k))
-        assert index.profile_read()["rescored_tiles_last"] > 0
+    for flat in (1, 0):
+        index = _idx(ip, ix, dt, N, options={"sample_p": 1, "flat": flat})
+        index.profile_enable(True)
+        for k in (100, 2048):
+            got = index.search(q, k)
+            _exact(got, oracle.search_c(N, ip, ix, dt, q, k))
+            assert index.profile_read()["rescored_tiles_last"] > 0
+            assert index.last_dispatch()["kernels"] == {"flat_all" if flat else "wave_all"}
 
 
 def test_search_device_torch(gpu):
@@ -344,36 +402,81 @@ def test_config3_full_batch_parity(gpu):
     assert np.array_equal(d2, docs) and np.array_equal(s2.view(np.uint32), scores.view(np.uint32))
 
 
-@pytest.mark.parametrize("variant", [
-    {}, {"BM25_SAMPLE_P": "1"}, {"BM25_SAMPLE_P": "2"}, {"BM25_SAMPLE_P": "16"},
-    {"BM25_LIST_CAP": "8"}, {"BM25_TILE_SHIFT": "10", "BM25_LIST_CAP": "40"},
-    {"BM25_NO_PIPE": "1"}, {"BM25_NO_PIPE": "1", "BM25_LIST_CAP": "8"},
-    {"BM25_SEGMENTS": "sparse"}, {"BM25_SEGMENTS": "sparse", "BM25_SAMPLE_P": "1"},
-    {"BM25_SEGMENTS": "sparse", "BM25_NO_BAND": "1"},
-    {"BM25_SEGMENTS": "sparse", "BM25_LIST_CAP": "8", "BM25_TILE_SHIFT": "10"},
-    {"BM25_FLAT": "0"}, {"BM25_FLAT": "0", "BM25_SEGMENTS": "sparse"},
-    {"BM25_FLAT_BW": "1"}, {"BM25_FLAT_BW": "2", "BM25_SEGMENTS": "sparse"},
-    {"BM25_FLAT_BW": "4", "BM25_SAMPLE_P": "2"},
-])
-def test_kernel_variants_bit_exact(gpu, variant, monkeypatch):
-    """Every search configuration gives the oracle's bits: sampling strides
-    (1 = one exact pass over every tile), and tiny candidate lists that force
-    queries through the exact fallback stage."""
-    for key, val in variant.items():
-        monkeypatch.setenv(key, val)
+def _sample_p(ntiles, k, W=1, pmax=8):
+    """The sampling stride sample_geom picks (bm25mi_kernels.hip): the first
+    P = pmax, pmax / 2, ... 2 whose sample of m = 1, 2 or 4 keys per sample
+    tile holds >= 2k keys; 1 (the exact pass) otherwise."""
+    P = 64
+    while P >= 2:
+        if P <= pmax and ntiles >= 2 * P:
+            G = 8 if ntiles >= 4 * 8 * P else 1
+            nS = (ntiles // (G * P)) * G + min(ntiles % (G * P), G)
+            if any(nS * m * W >= 2 * k for m in (1, 2, 4)):
+                return P
+        P //= 2
+    return 1
+
+
+# (options, segment table)
+VARIANTS = [
+    ({}, "dense"), ({"sample_p": 1}, "dense"), ({"sample_p": 2}, "dense"),
+    ({"sample_p": 16}, "dense"), ({"list_cap": 8}, "dense"), ({"flat": 0}, "dense"),
+    ({"flat": 0, "list_cap": 8}, "dense"), ({"flat": 0, "sample_p": 1}, "dense"),
+    ({}, "sparse"), ({"sample_p": 1}, "sparse"), ({"list_cap": 8}, "sparse"),
+    ({"flat": 0}, "sparse"), ({"flat_bw": 1}, "dense"), ({"flat_bw": 2}, "sparse"),
+    ({"flat_bw": 4, "sample_p": 2}, "dense"), ({"flat_bw": 8, "list_cap": 40}, "sparse"),
+    ({"claim_ch": 4, "claim_m": 1}, "dense"), ({"items_per_wave": 1000}, "dense"),
+]
+
+
+@pytest.mark.parametrize("T", [8, 16])
+@pytest.mark.parametrize("opts,segments", VARIANTS)
+def test_kernel_variants_bit_exact(gpu, opts, segments, T):
+    """Every search configuration gives the oracle's bits, and the search
+    reports that it ran the kernels the configuration selects
+    (bm25_search_dispatch): sampling strides (1 = one exact pass over every
+    tile), both score kernels, forced item widths, tiny candidate lists that
+    send queries through the exact fallback stage, both segment tables.
+    Options are set on the handle after it is built: they apply per search."""
     rng = np.random.default_rng(21)
-    N, V = 150_000, 900
+    N, V = 400_000, 900
     ip, ix, dt = _rand_index(rng, N, V, 20_000)
-    q = rng.integers(-1, V, size=(70, 8)).astype(np.int32)
+    q = rng.integers(-1, V, size=(70, T)).astype(np.int32)
     q[3, :] = -1
     q[4, 2:] = q[4, 1]
-    index = _idx(ip, ix, dt, N)
+    index = _idx(ip, ix, dt, N, segments=segments)
+    _exact(index.search(q, 7), oracle.search_c(N, ip, ix, dt, q, 7))  # defaults first
+    assert index.last_dispatch()["kernels"] == FLAT_SAMPLED
+    for name, val in opts.items():
+        index.set_option(name, val)
+        assert index.get_option(name) == val
+    flat = opts.get("flat", 1)
+    ntiles = index.info()["n_tiles"]
     fallback = 0
     for k in (1, 7, 100):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+        d = index.last_dispatch()
+        P = _sample_p(ntiles, k, 1, opts.get("sample_p", 8))
+        want = (FLAT_SAMPLED if flat else WAVE_SAMPLED) if P > 1 else \
+            {"flat_all" if flat else "wave_all"}
+        assert d["kernels"] == want and d["sample_p"] == P, (k, d, want, P)
+        if flat:
+            assert d["term_lanes"] == (8 if T == 8 else 16)
+            phase = "rest" if P > 1 else "all"
+            if "flat_bw" in opts:
+                assert d["band_tiles"][phase] == min(opts["flat_bw"], 64 // d["term_lanes"])
         fallback += index.search_stats()["fallback_queries"]
-    if "BM25_LIST_CAP" in variant:
+    if "list_cap" in opts:
         assert fallback > 0
+
+
+def test_options_rejected(gpu):
+    ip = np.array([0, 1], np.int32)
+    index = _idx(ip, np.array([0], np.int32), np.array([1.0], np.float32), 1)
+    for name, val in (("flat", 2), ("flat_bw", 3), ("sample_p", 3), ("claim_m", 9),
+                      ("nope", 1)):
+        with pytest.raises(ValueError):
+            index.set_option(name, val)
 
 
 def test_sharded_index_multi_shard_one_process(gpu):
@@ -757,3 +860,124 @@ def test_config5_shape_int64_shards_sparse(gpu, tmp_path, monkeypatch):
     merge_topk_device(0, lists_d, lists_s, W, len(q), cfg.k, md, ms, st)
     torch.cuda.synchronize()
     _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)
+
+
+# ------------------------------------------------ configs 4 and 5 in full
+def _protocol_search(shards, dq, k, sdm):
+    """bm25mi.dist.sharded_search (the bench's N > 1 step) over doc shards
+    held by this process, the two all-gathers replaced by concatenation;
+    returns the merged [Q, k] (docs, scores) on the host."""
+    import torch
+    from bm25mi.dist import sharded_search
+    from bm25mi.index import merge_topk_device
+    W, Q = len(shards), dq.shape[0]
+    st = torch.cuda.current_stream()
+    keys = []
+    for sh in shards:
+        S = sh.sample_width(k, W, sdm)
+        kk = torch.zeros((Q, max(S, 1)), dtype=torch.int64, device="cuda")
+        if S > 0:
+            sh.search_sample_device(dq, k, W, sdm, kk, st)
+        keys.append(kk)
+    all_keys = torch.stack(keys)
+
+    class Ex:
+        world = W
+
+        def __call__(self, _):
+            return all_keys
+
+    lists_d = torch.empty((W, Q, k), dtype=torch.int32, device="cuda")
+    lists_s = torch.empty((W, Q, k), dtype=torch.float32, device="cuda")
+    for r, sh in enumerate(shards):
+        sharded_search(sh, dq, k, sdm, lists_d[r], lists_s[r], None, st, exchange=Ex())
+    md = torch.empty((Q, k), dtype=torch.int32, device="cuda")
+    ms = torch.empty((Q, k), dtype=torch.float32, device="cuda")
+    merge_topk_device(0, lists_d, lists_s, W, Q, k, md, ms, st)
+    torch.cuda.synchronize()
+    return md.cpu().numpy(), ms.cpu().numpy()
+
+
+def test_config4_c3_index_eight_shards_full_batch(gpu):
+    """Config 4 at its own workload: the headline 10M-doc / 640M-posting
+    index doc-sharded 8 ways, all 1024 queries bit-exact vs the oracle on the
+    whole collection — (i) bm25_sharded_* (eight shards on cuda:0, global
+    threshold, peer-copied keys and lists, HIP merge); (ii) the
+    multi-process protocol of bench.py's N > 1 step (bm25mi.dist.
+    sharded_search over the per-rank shards the bench generates)."""
+    import torch
+    from bm25mi import synth
+    from bm25mi.index import GpuIndex, ShardedIndex
+    cfg = synth.CONFIGS["c3"]
+    ip, ix, dt = synth.make_index(cfg, threads=16)
+    q = synth.make_queries(cfg)
+    _progress("c4: index generated")
+    ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k, threads=16)
+    _progress("c4: oracle done")
+    sh = ShardedIndex(ip, ix, dt, cfg.n_docs, devices=[0] * 8)
+    assert len(sh.shards()) == 8
+    _progress("c4: 8 shards built")
+    _exact(sh.search(q, cfg.k), ref)
+    sh.close()
+    del ip, ix, dt
+    _progress("c4: bm25_sharded_search bit-exact")
+    W = 8
+    bounds = [synth.shard_bounds(cfg.n_docs, W, r) for r in range(W)]
+    sdm = max(hi - lo for lo, hi in bounds)
+    shards = []
+    for lo, hi in bounds:
+        shards.append(GpuIndex(*synth.make_index(cfg, lo, hi, threads=16), hi - lo, doc_offset=lo))
+        _progress(f"c4: rank shard [{lo}, {hi}) built")
+    _exact(_protocol_search(shards, torch.from_numpy(q).cuda(), cfg.k, sdm), ref)
+    d = shards[0].last_dispatch()
+    assert d["kernels"] == FLAT_SAMPLED, d
+    for s in shards:
+        s.close()
+
+
+@pytest.mark.parametrize("segments", ["dense", "sparse"])
+def test_config5_rank_shard_full_batch(gpu, segments):
+    """Config 5 at its own per-rank workload: one rank's doc shard of the
+    100M-doc / 1M-term / 6.4B-posting collection (12.5M docs, ~800M
+    postings, the global ids of rank 3: doc_offset 37.5M), all 1024 queries
+    bit-exact vs the oracle on that shard, on both segment tables (dense: 24
+    GB, the bench's; sparse: tile lists + the per-search table)."""
+    from bm25mi import synth
+    cfg = synth.CONFIGS["c5"]
+    lo, hi = synth.shard_bounds(cfg.n_docs, 8, 3)
+    ip, ix, dt = synth.make_index(cfg, lo, hi, threads=16)
+    assert ip.dtype == np.int64 and int(ip[-1]) > 700_000_000
+    q = synth.make_queries(cfg)
+    _progress(f"c5: rank shard [{lo}, {hi}) generated, nnz {int(ip[-1])}")
+    rd, rs = oracle.search_c(hi - lo, ip, ix, dt, q, cfg.k, threads=16)
+    _progress("c5: oracle done")
+    index = _idx(ip, ix, dt, hi - lo, doc_offset=lo, segments=segments)
+    _progress(f"c5: {segments} index built")
+    assert index.info()["sparse"] == (segments == "sparse")
+    _exact(index.search(q, cfg.k), (rd + lo, rs))
+    assert index.last_dispatch()["kernels"] == FLAT_SAMPLED
+    assert index.search_stats()["fallback_queries"] == 0
+    index.close()
+
+
+def test_rccl_all_gather_branch(gpu):
+    """bm25mi.dist's device all-gather (the RCCL branch: nccl backend,
+    all_gather_into_tensor on the search stream) on a real one-rank RCCL
+    communicator: shape [W, ...], rank-major, the packed [W, 2, Q, k] list
+    layout the merge reads."""
+    import torch
+    import torch.distributed as dist
+    from bm25mi.dist import _all_gather, gather_keys
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        pk = torch.arange(2 * 5 * 7, dtype=torch.int32, device="cuda").view(2, 5, 7)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            g = _all_gather(pk)
+            kk = gather_keys(torch.arange(5 * 3, dtype=torch.int64, device="cuda").view(5, 3))
+        s.synchronize()
+        assert tuple(g.shape) == (1, 2, 5, 7) and g.is_contiguous() and torch.equal(g[0], pk)
+        assert tuple(kk.shape) == (1, 5, 3) and int(kk[0, 4, 2]) == 14
+    finally:
+        dist.destroy_process_group()
