@@ -239,10 +239,10 @@ __device__ __forceinline__ void add_group(const IndexArgs& a, int64_t beg, uint3
       if (sf[j] < 0) break;
       const bool live = r0 + 64u * j + lane < total;
       if (sf[j] == sl[j]) {
-        if (live) lds_add(acc + dl[j], v[j]);
+        if (live) lds_add(acc + (dl[j] >> 2), v[j]);
       } else {
         for (int sc = sf[j]; sc <= sl[j]; ++sc)
-          if (live && ts[j] == sc) lds_add(acc + dl[j], v[j]);
+          if (live && ts[j] == sc) lds_add(acc + (dl[j] >> 2), v[j]);
       }
     }
   }
@@ -706,8 +706,6 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
 #ifndef BM25_FR_S
 #define BM25_FR_S 8
 #endif
-constexpr uint32_t kDeadSid = 0xFFFFFFFFu;   // padding row: no adds, no tile
-constexpr uint32_t kNoTag = 0xFFFFFFFFu;     // accumulator holds no tile
 
 #ifndef BM25_FLAT_WPE
 #define BM25_FLAT_WPE 5
@@ -733,10 +731,20 @@ struct FlatDesc {   // lane tile * 2^TL + term: the term's segment in the tile (
   uint32_t sk;      // REST: score-key half of the tile's best sample key (sample tiles)
 };
 
+// Row word of the process side: the row's valid positions [lo, hi) of its
+// 128 (position p = lane p / 2, slot p % 2) as lane ranges — slot 0: lanes
+// [lo, lo + n0), slot 1: lanes [0, n1) — and whether the row starts a tile
+// (and which tile of its item).
+constexpr uint32_t kRowNewTile = 1u << 17;
+__device__ __forceinline__ uint32_t row_lo(uint32_t w) { return w & 1u; }
+__device__ __forceinline__ uint32_t row_n0(uint32_t w) { return (w >> 1) & 0xFFu; }
+__device__ __forceinline__ uint32_t row_n1(uint32_t w) { return (w >> 9) & 0xFFu; }
+__device__ __forceinline__ uint32_t row_tile(uint32_t w) { return (w >> 18) & 0x3Fu; }
+
 struct FlatTab {    // one chunk of an item's rows: lane r = row j0 + r
   uint32_t base;    // even posting index of the row's first pair (0: dead row)
-  uint32_t pk;      // valid postings [lo, hi) of the row's 128 (lo = pk & 1, hi = pk >> 1)
-  uint32_t sid;     // (item serial << 6) | segment lane; kDeadSid: padding
+  uint32_t w;       // row word (above); 0: padding row
+  uint32_t last;    // (uniform) tile index of the chunk's row 63 (the next chunk's predecessor)
 };
 
 struct FlatCtx {    // the item a chunk (or the accumulator's tile) belongs to
@@ -745,10 +753,13 @@ struct FlatCtx {    // the item a chunk (or the accumulator's tile) belongs to
 };
 
 // Rows [j0, j0 + 64) of an item whose segment lane s holds segment
-// [sb, sb + sl), rows [excl, incl) of the item.
+// [sb, sb + sl), rows [excl, incl) of the item; prev = tile index of row
+// j0 - 1 (kNoTile at the item's first chunk: its first row starts a tile).
+constexpr uint32_t kNoTile = 0xFFFFFFFFu;
+template <int TL>
 __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t incl,
                                               uint32_t excl, uint32_t total, uint32_t j0,
-                                              uint32_t ser) {
+                                              uint32_t prev) {
   const uint32_t lane = lane_id();
   const uint32_t j = j0 + lane;
   int pos = 0;  // segments ending at or before row j (binary lifting)
@@ -767,8 +778,15 @@ __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t
   // row positions p of the segment: p + base in [b, b + l)
   const uint32_t rlo = k == 0u ? (b & 1u) : 0u;
   const uint32_t rhi = min(128u, (b & 1u) + l - 128u * k);
-  t.pk = (in && l != 0u) ? (rlo | (rhi << 1)) : 1u;
-  t.sid = in ? (ser << 6) | (uint32_t)pos : kDeadSid;
+  // slot 0 of lane l holds position 2l: valid for lanes [rlo, ceil(rhi / 2));
+  // slot 1 holds 2l + 1: lanes [0, floor(rhi / 2))
+  const uint32_t masks = (in && l != 0u) ? (rlo | ((((rhi + 1u) >> 1) - rlo) << 1) | ((rhi >> 1) << 9))
+                                         : 0u;
+  const uint32_t tile = (uint32_t)pos >> TL;
+  uint32_t tp = (uint32_t)__shfl_up((int)tile, 1, 64);
+  if (lane == 0u) tp = prev;
+  t.w = masks | ((in && tile != tp) ? kRowNewTile : 0u) | (tile << 18);
+  t.last = lane_u32(tile, 63);
   return t;
 }
 
@@ -791,7 +809,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   constexpr uint32_t kTileMask = (64u >> TL) - 1u;           // tile of a segment lane
   __shared__ __attribute__((aligned(16))) float acc[D + 64];
   const uint32_t lane = lane_id();
-  const uint32_t trash = (uint32_t)D + lane;  // this lane's always-zero slot
+  const uint32_t trash = ((uint32_t)D + lane) * 4u;  // byte offset of this lane's always-zero slot
   // stage queries: the fallback stage (ALL) reads its count on the device
   const int32_t nq = (PH == kAll && nq_dev) ? uniform(*nq_dev) : nq_host;
   const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
@@ -895,7 +913,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // ---- the issue side's item: its segments (lane s = tile * TT + term) and
   // row numbering; the item prefetch pipeline one and two items ahead
   uint32_t iSb = 0, iSl = 0, iIncl = 0, iExcl = 0;
-  uint32_t iTotal = 0, iR = 0, iJ0 = 0, iSer = 0;
+  uint32_t iTotal = 0, iR = 0, iJ0 = 0, iPrev = kNoTile;
   FlatCtx ctxI{0, 0, 0ull};
   FlatCur nx, nx2;
   FlatDesc dN;
@@ -921,7 +939,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     if ((R & 63u) != 0u && (R & 63u) < (uint32_t)kFR) R += (uint32_t)kFR - (R & 63u);
     iR = R;
     iJ0 = 0;
-    iSer = (iSer + 1u) & 0x3FFFFFFu;  // tags of consecutive items differ
+    iPrev = kNoTile;  // the item's first row starts a tile
     ctxI.q = nx.q;
     ctxI.b = nx.b;
     ctxI.th = thN;
@@ -956,24 +974,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   auto next_chunk = [&]() {  // tI <- the chunk after it (or the dead tail)
     if (iJ0 + 64u < iR) {
       iJ0 += 64u;
+      iPrev = tI.last;
     } else if (items_left && nx.rit < ngi) {
       enter_item();
     } else {
       items_left = false;
       iDead = true;
       tI.base = 0u;
-      tI.pk = 1u;
-      tI.sid = kDeadSid;
+      tI.w = 0u;
       nI = 0x7FFFFFFFu;
       il = 0;
       return;
     }
-    tI = flat_chunk(iSb, iSl, iIncl, iExcl, iTotal, iJ0, iSer);
+    tI = flat_chunk<TL>(iSb, iSl, iIncl, iExcl, iTotal, iJ0, iPrev);
     nI = min(64u, iR - iJ0);
     il = 0;
   };
   enter_item();
-  tI = flat_chunk(iSb, iSl, iIncl, iExcl, iTotal, 0u, iSer);
+  tI = flat_chunk<TL>(iSb, iSl, iIncl, iExcl, iTotal, 0u, iPrev);
   nI = min(64u, iR);
   il = 0;
 
@@ -993,28 +1011,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   for (int s = 0; s < kFR; ++s) issue(s);  // the first chunk holds >= kFR rows
 
   // process side
-  uint32_t tPpk = tI.pk, tPsid = tI.sid;  // the process side's chunk (no bases)
+  uint32_t tPw = tI.w;  // the process side's chunk (row words only)
   uint32_t nP = nI, pl = 0;
   FlatCtx ctxP = ctxI, ctxE = ctxI;
-  auto thf_of = [&](uint64_t th) -> float {
-    return (PH == kRest && a.nonneg && th_positive(th)) ? key_score((uint32_t)(th >> 32))
-                                                         : __builtin_nanf("");
-  };
-  float thfP = thf_of(ctxP.th);
-  uint32_t curTag = kNoTag;
-  uint64_t hit = 0;
+  uint32_t curTi = kNoTile;  // the accumulator's tile (index in item ctxE), kNoTile: none
+  // REST: the running maximum of the tile's sums (each doc's running sums
+  // only grow on a non-negative index, so the tile holds a key >= theta only
+  // if this reaches theta's score)
+  float hmax = 0.f;
   bool done = false;
 
   auto epilogue = [&]() {
-    const int32_t ti = ctxE.b * BW + (int32_t)(curTag & kTileMask);
+    const int32_t ti = ctxE.b * BW + (int32_t)curTi;
     const int64_t tile = tile_of32<PH>((uint32_t)ti, (uint32_t)P, (uint32_t)G);
     if constexpr (PH == kRest) {
       const bool flagged = a.nonneg && th_positive(ctxE.th);
-      if (flagged && hit == 0)
+      if (flagged && __ballot(hmax >= key_score((uint32_t)(ctxE.th >> 32))) == 0)
         zero_acc<S>(acc);
       else
         emit_rest<S>(acc, tile, a.n_docs, ctxE.th, list + (int64_t)ctxE.q * C,
                      list_cnt + ctxE.q, C);
+      hmax = 0.f;
     } else if constexpr (PH == kAll) {
       select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + (int64_t)ctxE.q * cstride + tile * kTileM);
     } else {
@@ -1026,21 +1043,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     }
   };
 
-  // the current row (its slot already consumed): masked slots and scores,
-  // the accumulator values read one step early, its segment id
-  uint32_t sc0, sc1, sidC;
+  // the current row (its slot already consumed): masked slot byte offsets
+  // and scores, the accumulator values read one step early, its row word
+  uint32_t sc0, sc1, wC;
   float ac0, ac1, xc0, xc1;
+  auto lds_at = [&](uint32_t off) -> float& {
+    return *reinterpret_cast<float*>(reinterpret_cast<char*>(acc) + off);
+  };
   auto prepare = [&](int s) {  // row pl of the process chunk, from slot s
-    sidC = lane_u32(tPsid, (int)pl);
-    const uint32_t pk = lane_u32(tPpk, (int)pl);
-    const uint32_t p0 = 2u * lane, rhi = pk >> 1;
-    const bool m0 = p0 >= (pk & 1u) && p0 < rhi, m1 = p0 + 1u < rhi;
+    wC = lane_u32(tPw, (int)pl);
+    const bool m0 = lane - row_lo(wC) < row_n0(wC), m1 = lane < row_n1(wC);
     sc0 = m0 ? (ldR[s] & 0xFFFFu) : trash;
     sc1 = m1 ? (ldR[s] >> 16) : trash;
     ac0 = m0 ? v0R[s] : 0.f;
     ac1 = m1 ? v1R[s] : 0.f;
-    xc0 = acc[sc0];
-    xc1 = acc[sc1];
+    xc0 = lds_at(sc0);
+    xc1 = lds_at(sc1);
   };
   prepare(0);
 
@@ -1048,28 +1066,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // s (consumed by the previous step), row r + 1 is prepared from slot s + 1
   auto step = [&](int s) {
     issue(s);
-    if (sidC != kDeadSid) {
-      const uint32_t tag = sidC >> TL;
-      if (tag != curTag) {
-        if (curTag != kNoTag) epilogue();
-        hit = 0;
-        curTag = tag;
-        ctxE = ctxP;
-        xc0 = 0.f;  // read before the epilogue cleared the accumulator
-        xc1 = 0.f;
-      }
+    if (wC & kRowNewTile) {
+      if (curTi != kNoTile) epilogue();
+      curTi = row_tile(wC) & kTileMask;
+      ctxE = ctxP;
+      xc0 = 0.f;  // read before the epilogue cleared the accumulator
+      xc1 = 0.f;
     }
     const float y0 = xc0 + ac0, y1 = xc1 + ac1;
-    acc[sc0] = y0;
-    acc[sc1] = y1;
-    if (PH == kRest) hit |= __ballot(fmaxf(y0, y1) >= thfP);
+    lds_at(sc0) = y0;
+    lds_at(sc1) = y1;
+    if (PH == kRest) hmax = fmaxf(hmax, fmaxf(y0, y1));
     if (++pl == nP) {  // the process side enters the issue side's chunk
-      tPpk = tI.pk;
-      tPsid = tI.sid;
+      tPw = tI.w;
       nP = nI;
       pl = 0;
       ctxP = ctxI;
-      thfP = thf_of(ctxP.th);
       done = iDead;
     }
     prepare((s + 1) % kFR);
@@ -1079,7 +1091,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
 #pragma unroll
     for (int s = 0; s < kFR; ++s) step(s);
   }
-  if (curTag != kNoTag) epilogue();
+  if (curTi != kNoTile) epilogue();
 }
 
 // ---------------------------------------------------------------------------
@@ -1196,7 +1208,7 @@ __global__ __launch_bounds__(256) void build_tables_kernel(
       const int32_t dp = p > a0 ? indices[p - 1] : -1;
       const bool ok = d >= 0 && (int64_t)d < n_docs && d > dp;
       if (!ok) atomicOr(err, 1);
-      ldoc[p] = (uint16_t)((uint32_t)d & mask);  // tile-local doc = LDS slot
+      ldoc[p] = (uint16_t)(((uint32_t)d & mask) << 2);  // LDS byte offset of the doc's slot
       if (heavy && ok) {
         const int64_t tp = dp >= 0 ? ((int64_t)dp >> S) : -1;
         const int64_t tc = (int64_t)d >> S;
@@ -1243,7 +1255,7 @@ __global__ __launch_bounds__(256) void count_tiles_kernel(
       const int32_t dp = p > a0 ? indices[p - 1] : -1;
       const bool ok = d >= 0 && (int64_t)d < n_docs && d > dp;
       if (!ok) atomicOr(err, 1);
-      ldoc[p] = (uint16_t)((uint32_t)d & mask);
+ ldoc[p] = (uint16_t)(((uint32_t)d & mask) << 2);
       n += (dp < 0 || (d >> S) != (dp >> S)) ? 1u : 0u;
     }
     const uint32_t tot = wave_incl_scan(n);
@@ -1286,6 +1298,9 @@ __global__ __launch_bounds__(256) void fill_tiles_kernel(
 // Merge: one workgroup per query, bitonic sort of u64 keys in LDS.
 // ---------------------------------------------------------------------------
 constexpr int kMergeNT = 1024;
+// Workgroups of the fallback stage's launches (its queries are counted on the
+// device and are usually none; the launches must stay cheap).
+constexpr int kFallbackBlocks = 64;
 constexpr int kMaxFlagBits = 65536;  // tiles per query addressable by the flag bitmap
 
 __device__ __forceinline__ int next_pow2(int64_t x) {
@@ -1525,14 +1540,11 @@ __device__ __forceinline__ int64_t stage_nq(const Stage& sg) {
   return sg.nq_dev ? (int64_t)*sg.nq_dev : (int64_t)sg.nq_host;
 }
 
-__global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
-    Stage sg, int32_t k, int64_t maxflag, int64_t doc_offset, int64_t n_docs, Workspace ws,
-    int32_t* __restrict__ docs, float* __restrict__ scores) {
-  __shared__ uint64_t keys[kMergeP];
-  __shared__ int32_t s_nflag, s_cnt;
-  __shared__ uint32_t zf_bits[2 * kMaxK / 32];
-  const int64_t qi = blockIdx.x;
-  if (qi >= stage_nq(sg)) return;
+// One query of merge_first_kernel (the block's shared arrays passed in).
+__device__ void merge_first_one(const Stage& sg, int32_t k, int64_t maxflag, int64_t doc_offset,
+                                int64_t n_docs, const Workspace& ws, int32_t* __restrict__ docs,
+                                float* __restrict__ scores, int64_t qi, uint64_t* keys,
+                                int32_t& s_nflag, int32_t* s_cnt, uint32_t* zf_bits) {
   const int64_t q = sg.qmap ? (int64_t)sg.qmap[qi] : qi;
   const int32_t cnt = sg.list ? sg.list_cnt[qi] : 0;
   if (cnt > sg.C) {  // the list overflowed: exact fallback stage
@@ -1547,7 +1559,7 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
   // theta (sampled stage): k sample candidates are >= it, so nothing below it
   // can reach the top-k; every list entry is above it
   topk_compact(SrcCat{c, sg.list ? sg.list + qi * sg.C : nullptr, sg.nt * kTileM},
-               sg.nt * kTileM + cnt, k, sg.theta ? sg.theta[qi] : 0ull, keys, &s_cnt);
+               sg.nt * kTileM + cnt, k, sg.theta ? sg.theta[qi] : 0ull, keys, s_cnt);
   if (sg.theta && sg.theta[qi] == kZeroFillTheta && cnt < k) {
     // the list holds every positive doc: complete it with the smallest doc ids
     // outside it (all < k + cnt), score 0; a shard holding fewer than k docs
@@ -1598,13 +1610,26 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
   if (nf == 0) write_result(keys, k, q, doc_offset, docs, scores);
 }
 
-__global__ __launch_bounds__(kMergeNT) void merge_final_kernel(
-    Stage sg, int32_t k, int64_t maxflag, int64_t doc_offset, Workspace ws,
+// One block per stage query, or (the fallback stage, whose query count is
+// read on the device and usually 0) a few blocks looping over them.
+__global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
+    Stage sg, int32_t k, int64_t maxflag, int64_t doc_offset, int64_t n_docs, Workspace ws,
     int32_t* __restrict__ docs, float* __restrict__ scores) {
   __shared__ uint64_t keys[kMergeP];
-  __shared__ uint32_t bits[kMaxFlagBits / 32];
-  const int64_t qi = blockIdx.x;
-  if (qi >= stage_nq(sg)) return;
+  __shared__ int32_t s_nflag, s_cnt;
+  __shared__ uint32_t zf_bits[2 * kMaxK / 32];
+  const int64_t nq = stage_nq(sg);
+  for (int64_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    __syncthreads();  // the previous query's shared state is consumed
+    merge_first_one(sg, k, maxflag, doc_offset, n_docs, ws, docs, scores, qi, keys, s_nflag,
+                    &s_cnt, zf_bits);
+  }
+}
+
+__device__ void merge_final_one(const Stage& sg, int32_t k, int64_t maxflag, int64_t doc_offset,
+                                const Workspace& ws, int32_t* __restrict__ docs,
+                                float* __restrict__ scores, int64_t qi, uint64_t* keys,
+                                uint32_t* bits) {
   const int nf = ws.nflag[qi];
   if (nf == 0) return;
   const int64_t q = sg.qmap ? (int64_t)sg.qmap[qi] : qi;
@@ -1621,6 +1646,18 @@ __global__ __launch_bounds__(kMergeNT) void merge_final_kernel(
                ws.cand2 + qi * maxflag * (int64_t)k, bits, sg.nt * kTileM, cnt};
   topk_of(src, sg.nt * kTileM + cnt + (int64_t)nf * k, k, keys);
   write_result(keys, k, q, doc_offset, docs, scores);
+}
+
+__global__ __launch_bounds__(kMergeNT) void merge_final_kernel(
+    Stage sg, int32_t k, int64_t maxflag, int64_t doc_offset, Workspace ws,
+    int32_t* __restrict__ docs, float* __restrict__ scores) {
+  __shared__ uint64_t keys[kMergeP];
+  __shared__ uint32_t bits[kMaxFlagBits / 32];
+  const int64_t nq = stage_nq(sg);
+  for (int64_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    __syncthreads();
+    merge_final_one(sg, k, maxflag, doc_offset, ws, docs, scores, qi, keys, bits);
+  }
 }
 
 __global__ __launch_bounds__(kMergeNT) void merge_lists_kernel(
@@ -1788,7 +1825,8 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
   a.seg_zero = Qb * ((ix.ntiles + 7) >> 3) * 8 * (1 << TL);
   const int64_t nt = PH == kSample ? sample_count(ix.ntiles, sg.P, sg.G) : ix.ntiles;
   auto go = [&](auto kern) {
-    const int grid = persistent_grid(kern, 64);
+    int grid = persistent_grid(kern, 64);
+    if (sg.nq_dev) grid = std::min(grid, 8 * kFallbackBlocks);  // fallback: usually no queries
     const int bw = flat_band(ix.opt, nt, sg.nq_host, grid, 64 >> TL, sg.nq_dev != nullptr);
     ix.disp.kernels |= PH == kSample ? kKFlatSample : (PH == kRest ? kKFlatRest : kKFlatAll);
     ix.disp.term_lanes = 1 << TL;
@@ -1830,7 +1868,8 @@ static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t T, int64_
   int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;
   (void)wctr;
   ix.disp.kernels |= PH == kSample ? kKWaveSample : (PH == kRest ? kKWaveRest : kKWaveAll);
-  const int grid = persistent_grid(score_wave_kernel<S, PH>, 64 * kWaves);
+  int grid = persistent_grid(score_wave_kernel<S, PH>, 64 * kWaves);
+  if (sg.nq_dev) grid = std::min(grid, 8 * kFallbackBlocks);
   hipLaunchKernelGGL((score_wave_kernel<S, PH>), dim3((unsigned)grid), dim3(64 * kWaves), 0, st,
                      args_of(ix), q, (int32_t)T, sg, ws.theta, sg.cand_out, ws.list, ws.list_cnt,
                      ws.list_cap);
@@ -2041,13 +2080,17 @@ template <int S>
 static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k, const Stage& sg,
                          const Workspace& ws, int32_t* docs, float* scores, hipStream_t st) {
   const int64_t maxflag = maxflag_for(k, sg.nt);
-  hipLaunchKernelGGL(merge_first_kernel, dim3((unsigned)sg.nq_host), dim3(kMergeNT), 0, st, sg,
-                     (int32_t)k, maxflag, ix.doc_offset, ix.n_docs, ws, docs, scores);
+  // the fallback stage (query count on the device, usually 0): a few blocks
+  const unsigned mgrid = (unsigned)(sg.nq_dev ? std::min<int64_t>(sg.nq_host, kFallbackBlocks)
+                                              : sg.nq_host);
+  hipLaunchKernelGGL(merge_first_kernel, dim3(mgrid), dim3(kMergeNT), 0, st, sg, (int32_t)k,
+                     maxflag, ix.doc_offset, ix.n_docs, ws, docs, scores);
   if (k > kTileM && sg.nt > 0) {  // tiles with exact top-4 candidates may need a rescore
-    hipLaunchKernelGGL(rescore_kernel<S>, dim3(256), dim3(kRescoreNT), 0, st, args_of(ix), q,
-                       (int32_t)T, (int32_t)k, maxflag, sg, ws);
-    hipLaunchKernelGGL(merge_final_kernel, dim3((unsigned)sg.nq_host), dim3(kMergeNT), 0, st, sg,
-                       (int32_t)k, maxflag, ix.doc_offset, ws, docs, scores);
+    hipLaunchKernelGGL(rescore_kernel<S>, dim3(sg.nq_dev ? kFallbackBlocks : 256),
+                       dim3(kRescoreNT), 0, st, args_of(ix), q, (int32_t)T, (int32_t)k, maxflag,
+                       sg, ws);
+    hipLaunchKernelGGL(merge_final_kernel, dim3(mgrid), dim3(kMergeNT), 0, st, sg, (int32_t)k,
+                       maxflag, ix.doc_offset, ws, docs, scores);
   }
 }
 
@@ -2057,8 +2100,9 @@ static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   select_stage<S_>(ix, q, T, k, main_stage(ix, Q, P, ws), ws, docs, scores, st);
   if (P == 1) return;
   // queries whose list overflowed: exact pass over every tile (usually none;
-  // the kernels read their count on the device and exit at once)
-  hipMemsetAsync(ws.counters, 0, 2 * sizeof(int32_t), st);
+  // the kernels read their count on the device and exit at once).  The
+  // rescore queue counters [0], [1] are still 0 from zero_search_kernel (the
+  // sampled main stage has no tile candidates to rescore).
   Stage fb = fallback_stage(ix, Q, ws);
   fb.ctr_region = 2;  // unused by the sampled search: zeroed by sample_s
   fb.ctr_zeroed = true;
