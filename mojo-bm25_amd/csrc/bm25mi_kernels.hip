@@ -736,6 +736,8 @@ struct FlatDesc {   // lane tile * 2^TL + term: the term's segment in the tile (
 // [lo, lo + n0), slot 1: lanes [0, n1) — and whether the row starts a tile
 // (and which tile of its item).
 constexpr uint32_t kRowNewTile = 1u << 17;
+constexpr uint32_t kRowNewItem = 1u << 24;   // the item's row 0 (a tile start unless the item is empty)
+constexpr uint32_t kRowDead = 1u << 25;      // past the wave's last item
 __device__ __forceinline__ uint32_t row_lo(uint32_t w) { return w & 1u; }
 __device__ __forceinline__ uint32_t row_n0(uint32_t w) { return (w >> 1) & 0xFFu; }
 __device__ __forceinline__ uint32_t row_n1(uint32_t w) { return (w >> 9) & 0xFFu; }
@@ -747,7 +749,7 @@ struct FlatTab {    // one chunk of an item's rows: lane r = row j0 + r
   uint32_t last;    // (uniform) tile index of the chunk's row 63 (the next chunk's predecessor)
 };
 
-struct FlatCtx {    // the item a chunk (or the accumulator's tile) belongs to
+struct FlatCtx {    // the item the accumulator's tile belongs to
   int32_t q, b;
   uint64_t th;
 };
@@ -785,7 +787,10 @@ __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t
   const uint32_t tile = (uint32_t)pos >> TL;
   uint32_t tp = (uint32_t)__shfl_up((int)tile, 1, 64);
   if (lane == 0u) tp = prev;
-  t.w = masks | ((in && tile != tp) ? kRowNewTile : 0u) | (tile << 18);
+  // (an item with no rows at all still marks its row 0: the process side
+  // counts items to find their contexts)
+  t.w = masks | ((in && tile != tp) ? kRowNewTile : 0u) | (tile << 18) |
+        (j == 0u ? kRowNewItem : 0u);
   t.last = lane_u32(tile, 63);
   return t;
 }
@@ -914,7 +919,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // row numbering; the item prefetch pipeline one and two items ahead
   uint32_t iSb = 0, iSl = 0, iIncl = 0, iExcl = 0;
   uint32_t iTotal = 0, iR = 0, iJ0 = 0, iPrev = kNoTile;
-  FlatCtx ctxI{0, 0, 0ull};
+  int32_t ctxV = 0, iPar = 0;
   FlatCur nx, nx2;
   FlatDesc dN;
   uint64_t thN = 0ull;
@@ -940,9 +945,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     iR = R;
     iJ0 = 0;
     iPrev = kNoTile;  // the item's first row starts a tile
-    ctxI.q = nx.q;
-    ctxI.b = nx.b;
-    ctxI.th = thN;
+    // the item's context for the process side: lanes 4 * parity + (q, b,
+    // theta lo, theta hi) of ctxV (items hold >= kFR rows, so at most two are
+    // between the process and the issue side)
+    {
+      const int32_t c4 = (int32_t)lane - 4 * iPar;
+      ctxV = c4 == 0 ? nx.q : c4 == 1 ? nx.b : c4 == 2 ? (int32_t)(uint32_t)thN
+           : c4 == 3 ? (int32_t)(uint32_t)(thN >> 32) : ctxV;
+    }
+    iPar ^= 1;
     // prefetch: descriptors of the item after, terms of the one after that
     FlatCur nx3 = next(nx2);
     dN = load_bdesc(nx2, tmN2);
@@ -968,7 +979,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   acc[D + lane] = 0.f;
 
   // issue table: the chunk the next issued row comes from
-  bool items_left = true, iDead = false;
+  bool items_left = true;
   FlatTab tI;
   uint32_t nI = 0, il = 0;
   auto next_chunk = [&]() {  // tI <- the chunk after it (or the dead tail)
@@ -979,9 +990,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       enter_item();
     } else {
       items_left = false;
-      iDead = true;
       tI.base = 0u;
-      tI.w = 0u;
+      tI.w = kRowDead;
       nI = 0x7FFFFFFFu;
       il = 0;
       return;
@@ -995,12 +1005,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   nI = min(64u, iR);
   il = 0;
 
-  // ring: slot s holds the raw loads of rows r == s (mod kFR)
-  uint32_t ldR[kFR];
+  // ring: slot s holds the raw loads and the row word of rows r == s (mod kFR)
+  uint32_t ldR[kFR], wR[kFR];
   float v0R[kFR], v1R[kFR];
   auto issue = [&](int s) {
     if (il == nI) next_chunk();
     const uint32_t base = lane_u32(tI.base, (int)il);
+    wR[s] = lane_u32(tI.w, (int)il);
     ldR[s] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)(lane * 4u), (int)(base * 2u), 0);
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)(lane * 8u), (int)(base * 4u), 0);
     v0R[s] = __uint_as_float((uint32_t)v[0]);
@@ -1011,9 +1022,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   for (int s = 0; s < kFR; ++s) issue(s);  // the first chunk holds >= kFR rows
 
   // process side
-  uint32_t tPw = tI.w;  // the process side's chunk (row words only)
-  uint32_t nP = nI, pl = 0;
-  FlatCtx ctxP = ctxI, ctxE = ctxI;
+  int32_t pPar = 1;  // parity of the process side's item (its first row flips it)
+  FlatCtx ctxE{0, 0, 0ull};
   uint32_t curTi = kNoTile;  // the accumulator's tile (index in item ctxE), kNoTile: none
   // REST: the running maximum of the tile's sums (each doc's running sums
   // only grow on a non-negative index, so the tile holds a key >= theta only
@@ -1050,8 +1060,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   auto lds_at = [&](uint32_t off) -> float& {
     return *reinterpret_cast<float*>(reinterpret_cast<char*>(acc) + off);
   };
-  auto prepare = [&](int s) {  // row pl of the process chunk, from slot s
-    wC = lane_u32(tPw, (int)pl);
+  auto prepare = [&](int s) {  // the row of slot s
+    wC = wR[s];
     const bool m0 = lane - row_lo(wC) < row_n0(wC), m1 = lane < row_n1(wC);
     sc0 = m0 ? (ldR[s] & 0xFFFFu) : trash;
     sc1 = m1 ? (ldR[s] >> 16) : trash;
@@ -1066,10 +1076,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // s (consumed by the previous step), row r + 1 is prepared from slot s + 1
   auto step = [&](int s) {
     issue(s);
+    if (wC & (kRowNewTile | kRowNewItem)) {
+      if (wC & kRowNewItem) pPar ^= 1;
+    }
     if (wC & kRowNewTile) {
       if (curTi != kNoTile) epilogue();
       curTi = row_tile(wC) & kTileMask;
-      ctxE = ctxP;
+      ctxE.q = __builtin_amdgcn_readlane(ctxV, 4 * pPar);
+      ctxE.b = __builtin_amdgcn_readlane(ctxV, 4 * pPar + 1);
+      ctxE.th = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(ctxV, 4 * pPar + 3) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane(ctxV, 4 * pPar + 2);
       xc0 = 0.f;  // read before the epilogue cleared the accumulator
       xc1 = 0.f;
     }
@@ -1077,13 +1093,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     lds_at(sc0) = y0;
     lds_at(sc1) = y1;
     if (PH == kRest) hmax = fmaxf(hmax, fmaxf(y0, y1));
-    if (++pl == nP) {  // the process side enters the issue side's chunk
-      tPw = tI.w;
-      nP = nI;
-      pl = 0;
-      ctxP = ctxI;
-      done = iDead;
-    }
+    done = (wC & kRowDead) != 0u;  // (rows past the last item add nothing)
     prepare((s + 1) % kFR);
   };
 
