@@ -814,7 +814,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   constexpr uint32_t kTileMask = (64u >> TL) - 1u;           // tile of a segment lane
   __shared__ __attribute__((aligned(16))) float acc[D + 64];
   const uint32_t lane = lane_id();
-  const uint32_t trash = ((uint32_t)D + lane) * 4u;  // byte offset of this lane's always-zero slot
+  // byte offset of this lane's trash slot: it holds -inf, so a masked lane
+  // needs no masked score (-inf + any finite score = -inf) and never raises
+  // the tile's running maximum
+  const uint32_t trash = ((uint32_t)D + lane) * 4u;
   // stage queries: the fallback stage (ALL) reads its count on the device
   const int32_t nq = (PH == kAll && nq_dev) ? uniform(*nq_dev) : nq_host;
   const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
@@ -976,7 +979,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   tmN2 = terms_of(nx2);
   for (int j = 0; j < D / 256; ++j)
     reinterpret_cast<float4*>(acc)[j * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-  acc[D + lane] = 0.f;
+  acc[D + lane] = -__builtin_inff();
 
   // issue table: the chunk the next issued row comes from
   bool items_left = true;
@@ -1065,8 +1068,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const bool m0 = lane - row_lo(wC) < row_n0(wC), m1 = lane < row_n1(wC);
     sc0 = m0 ? (ldR[s] & 0xFFFFu) : trash;
     sc1 = m1 ? (ldR[s] >> 16) : trash;
-    ac0 = m0 ? v0R[s] : 0.f;
-    ac1 = m1 ? v1R[s] : 0.f;
+    ac0 = v0R[s];  // masked lanes: a finite score of another posting, added to -inf
+    ac1 = v1R[s];
     xc0 = lds_at(sc0);
     xc1 = lds_at(sc1);
   };
@@ -1086,8 +1089,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       ctxE.b = __builtin_amdgcn_readlane(ctxV, 4 * pPar + 1);
       ctxE.th = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(ctxV, 4 * pPar + 3) << 32) |
                 (uint32_t)__builtin_amdgcn_readlane(ctxV, 4 * pPar + 2);
-      xc0 = 0.f;  // read before the epilogue cleared the accumulator
-      xc1 = 0.f;
+      // read before the epilogue cleared the accumulator (trash lanes keep -inf)
+      xc0 = sc0 == trash ? xc0 : 0.f;
+      xc1 = sc1 == trash ? xc1 : 0.f;
     }
     const float y0 = xc0 + ac0, y1 = xc1 + ac1;
     lds_at(sc0) = y0;
