@@ -93,6 +93,7 @@ void free_ws(Workspace& ws) {
   hipFree(ws.nflag);
   hipFree(ws.queue);
   hipFree(ws.counters);
+  hipFree(ws.slow);
   hipFree(ws.wctr);
   hipFree(ws.seg);
   ws = Workspace{};
@@ -193,8 +194,9 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMalloc(&ws.flag_tiles, sizeof(int32_t) * q * mf), "hipMalloc(flag_tiles)");
   HIP_TRY(hipMalloc(&ws.nflag, sizeof(int32_t) * q), "hipMalloc(nflag)");
   HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
-  HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * 4), "hipMalloc(counters)");
-  HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * 4), "hipMemset(counters)");
+  HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * kCounters), "hipMalloc(counters)");
+  HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * kCounters), "hipMemset(counters)");
+  HIP_TRY(hipMalloc(&ws.slow, sizeof(int32_t) * q), "hipMalloc(slow)");
   HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMalloc(wctr)");
   ws.cap_seg = need_seg;
   if (ws.cap_seg > 0) HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * ws.cap_seg), "hipMalloc(seg)");

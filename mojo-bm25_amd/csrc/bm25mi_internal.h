@@ -108,6 +108,8 @@ struct DevIndex {
   mutable Dispatch disp;  // written by the launchers (callers hold the handle's mutex)
 };
 
+constexpr int kCounters = 8;  // Workspace::counters
+
 struct Workspace {
   int64_t cap_q = 0, cap_k = 0;
   uint64_t* cand = nullptr;      // [Q][ntiles][kTileM] exact top-kTileM keys of sample (or all) tiles
@@ -120,8 +122,10 @@ struct Workspace {
   int32_t* flag_tiles = nullptr; // [Q][maxflag]
   int32_t* nflag = nullptr;      // [Q]
   int32_t* queue = nullptr;      // [Q*maxflag] items = qi*maxflag + i
-  int32_t* counters = nullptr;   // [0]/[1] rescore queue length / pop cursor,
-                                 // [2] fallback queries, [3] tiles re-scored this search
+  int32_t* counters = nullptr;   // [kCounters]: [0]/[1] rescore queue length / pop cursor,
+                                 // [2] fallback queries, [3] tiles re-scored this search,
+                                 // [4] queries left to the block merge (slow)
+  int32_t* slow = nullptr;       // [Q] those queries
   int32_t* wctr = nullptr;       // [kWctrRegions][kWctrInts] item-claim counters, zeroed per search
   uint64_t* seg = nullptr;       // sparse index: [Q][tiles/8][TT][8] segment of each (query,
                                  // term position, tile) (start | len << 32), built per search

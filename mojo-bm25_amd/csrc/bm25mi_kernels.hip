@@ -121,6 +121,8 @@ struct Stage {
   int32_t* fb_cnt;
   int32_t ctr_region;        // claim counters of the launch: ws.wctr + region * kWctrInts
   bool ctr_zeroed;           // ... already zeroed by the search's zero_search_kernel
+  bool remap;                // merges: qmap gives the batch row of every array (the
+                             // main stage's queries left to the block merge)
 };
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -1559,7 +1561,7 @@ __device__ void merge_first_one(const Stage& sg, int32_t k, int64_t maxflag, int
                                 int64_t n_docs, const Workspace& ws, int32_t* __restrict__ docs,
                                 float* __restrict__ scores, int64_t qi, uint64_t* keys,
                                 int32_t& s_nflag, int32_t* s_cnt, uint32_t* zf_bits) {
-  const int64_t q = sg.qmap ? (int64_t)sg.qmap[qi] : qi;
+  const int64_t q = (sg.qmap && !sg.remap) ? (int64_t)sg.qmap[qi] : qi;
   const int32_t cnt = sg.list ? sg.list_cnt[qi] : 0;
   if (cnt > sg.C) {  // the list overflowed: exact fallback stage
     if (threadIdx.x == 0) {
@@ -1633,10 +1635,136 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
   __shared__ int32_t s_nflag, s_cnt;
   __shared__ uint32_t zf_bits[2 * kMaxK / 32];
   const int64_t nq = stage_nq(sg);
-  for (int64_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+  for (int64_t i = blockIdx.x; i < nq; i += gridDim.x) {
     __syncthreads();  // the previous query's shared state is consumed
-    merge_first_one(sg, k, maxflag, doc_offset, n_docs, ws, docs, scores, qi, keys, s_nflag,
-                    &s_cnt, zf_bits);
+    merge_first_one(sg, k, maxflag, doc_offset, n_docs, ws, docs, scores,
+                    sg.remap ? (int64_t)sg.qmap[i] : i, keys, s_nflag, &s_cnt, zf_bits);
+  }
+}
+
+// Main stage of a sampled search, one wavefront per query (no barriers): the
+// query's list — every key >= theta of the non-sample tiles, ~P k keys —
+// is held in registers (kFastR per lane), the k-th largest key is found by a
+// radix selection (score half, then the doc half only among keys of that
+// score), the <= k keys at or above it are sorted in the wave's LDS slice
+// (bitonic) and written out.  Queries this cannot serve — an overflowed list
+// (the exact fallback stage, as merge_first), a list longer than 64 kFastR,
+// a zero-fill threshold with fewer than k keys — are queued for
+// merge_first_kernel (ws.slow).  Replaces the block-per-query sort of the
+// whole list (merge_first: 1024 threads, ~55 barrier-separated bitonic stages
+// over the padded list) for the common case.
+constexpr int kFastR = 32;      // list keys per lane held in registers
+constexpr int kFastMaxK = 1024; // largest k served (LDS: k keys per wave)
+
+__global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, int64_t doc_offset,
+                                                         Workspace ws, int32_t* __restrict__ docs,
+                                                         float* __restrict__ scores) {
+  __shared__ uint64_t sk[4][kFastMaxK];
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= sg.nq_host) return;  // wave-uniform; no barriers in this kernel
+  const uint32_t lane = lane_id();
+  uint64_t* keys = sk[threadIdx.x >> 6];
+  const int32_t cnt = sg.list_cnt[q];
+  const uint64_t th = sg.theta[q];
+  if (cnt > sg.C) {  // overflowed: exact fallback stage
+    if (lane == 0) {
+      ws.nflag[q] = 0;
+      sg.fb[atomicAdd(sg.fb_cnt, 1)] = (int32_t)q;
+    }
+    return;
+  }
+  if (cnt > 64 * kFastR || (th == kZeroFillTheta && cnt < k)) {
+    if (lane == 0) ws.slow[atomicAdd(ws.counters + 4, 1)] = (int32_t)q;
+    return;
+  }
+  const uint64_t* lst = sg.list + q * (int64_t)sg.C;
+  uint64_t key[kFastR];
+#pragma unroll
+  for (int j = 0; j < kFastR; ++j) {
+    const int i = j * 64 + (int)lane;
+    const uint64_t x = i < cnt ? lst[i] : 0ull;
+    key[j] = x >= th ? x : 0ull;  // (every list key is >= theta; key 0 = empty)
+  }
+  // kth = the k-th largest key (0: fewer than k keys, all of them are kept)
+  uint64_t kth = 0ull;
+  uint32_t n = 0;
+#pragma unroll
+  for (int j = 0; j < kFastR; ++j) n += key[j] != 0ull;
+  n = wave_sum_u32(n);
+  if (n > (uint32_t)k) {
+    uint32_t need = (uint32_t)k, hi = 0u;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t hm = ~0u << bit, cand = hi | (1u << bit);
+      uint32_t c = 0;
+#pragma unroll
+      for (int j = 0; j < kFastR; ++j) c += ((uint32_t)(key[j] >> 32) & hm) == cand;
+      const uint32_t tot = wave_sum_u32(c);
+      if (tot >= need) hi = cand;
+      else need -= tot;
+    }
+    // need = rank of the answer among the keys of score hi
+    uint32_t ties = 0;
+#pragma unroll
+    for (int j = 0; j < kFastR; ++j) ties += (uint32_t)(key[j] >> 32) == hi;
+    uint32_t lo = 0u;
+    if (wave_sum_u32(ties) > 1u) {
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t hm = ~0u << bit, cand = lo | (1u << bit);
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < kFastR; ++j)
+          c += ((uint32_t)(key[j] >> 32) == hi) & (((uint32_t)key[j] & hm) == cand);
+        const uint32_t tot = wave_sum_u32(c);
+        if (tot >= need) lo = cand;
+        else need -= tot;
+      }
+    } else {
+      uint32_t m = 0u;
+#pragma unroll
+      for (int j = 0; j < kFastR; ++j) m = (uint32_t)(key[j] >> 32) == hi ? (uint32_t)key[j] : m;
+      lo = wave_max_u32(m);
+    }
+    kth = ((uint64_t)hi << 32) | lo;
+    n = (uint32_t)k;
+  }
+  // the n kept keys (>= kth; unique: doc ids differ) -> LDS, sorted best first
+  const int m = next_pow2(n > 1u ? n : 2u);
+  uint32_t base = 0u;
+#pragma unroll
+  for (int j = 0; j < kFastR; ++j) {
+    const bool keep = key[j] != 0ull && key[j] >= kth;
+    const uint64_t b = __ballot(keep);
+    if (keep)
+      keys[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
+    base += (uint32_t)__popcll(b);
+  }
+  for (int i = (int)n + (int)lane; i < m; i += 64) keys[i] = 0ull;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (int size = 2; size <= m; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int ls = __builtin_ctz((unsigned)stride);
+      for (int i = (int)lane; i < (m >> 1); i += 64) {
+        const int a = ((i >> ls) << (ls + 1)) + (i & (stride - 1)), b2 = a + stride;
+        const bool desc = (a & size) == 0;
+        const uint64_t x = keys[a], y = keys[b2];
+        if ((x < y) == desc) {
+          keys[a] = y;
+          keys[b2] = x;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+  }
+  for (int i = (int)lane; i < k; i += 64) {
+    const uint64_t x = i < m ? keys[i] : 0ull;
+    if (x == 0ull) {  // padding (a shard holding fewer than k keys)
+      docs[q * k + i] = -1;
+      scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
+    } else {
+      docs[q * k + i] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)x) + doc_offset);
+      scores[q * k + i] = key_score((uint32_t)(x >> 32));
+    }
   }
 }
 
@@ -1999,7 +2127,7 @@ __global__ __launch_bounds__(256) void zero_search_kernel(uint64_t* __restrict__
   for (int64_t i = i0; i < nk; i += st) keys[i] = 0ull;
   for (int64_t i = i0; i < nw; i += st) wctr[i] = 0;
   for (int64_t i = i0; i < Q; i += st) list_cnt[i] = 0;
-  if (i0 < 4) counters[i0] = 0;
+  if (i0 < kCounters) counters[i0] = 0;
 }
 
 // SAMPLE pass: each query's S keys into keys[Q][S] (zero-padded); a copy
@@ -2033,7 +2161,7 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
                      hipStream_t st) {
   Stage sg = main_stage(ix, Q, g.P, ws);
   if (g.P == 1) {  // no sample pass ran: nothing was zeroed, no segment table built
-    hipMemsetAsync(ws.counters, 0, 4 * sizeof(int32_t), st);
+    hipMemsetAsync(ws.counters, 0, kCounters * sizeof(int32_t), st);
     if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, q, Q, T, ws, st);
     sg.ctr_region = 2;
     sg.ctr_zeroed = false;
@@ -2094,6 +2222,20 @@ template <int S>
 static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k, const Stage& sg,
                          const Workspace& ws, int32_t* docs, float* scores, hipStream_t st) {
   const int64_t maxflag = maxflag_for(k, sg.nt);
+  if (sg.theta && !sg.qmap && sg.nt == 0 && k <= kFastMaxK) {
+    // sampled main stage: one wavefront per query; the queries it leaves go
+    // to the block merge below (their count on the device, usually 0)
+    hipLaunchKernelGGL(merge_fast_kernel, dim3((unsigned)((sg.nq_host + 3) / 4)), dim3(256), 0,
+                       st, sg, (int32_t)k, ix.doc_offset, ws, docs, scores);
+    Stage sl = sg;
+    sl.qmap = ws.slow;
+    sl.nq_dev = ws.counters + 4;
+    sl.remap = true;
+    hipLaunchKernelGGL(merge_first_kernel, dim3((unsigned)std::min<int64_t>(sg.nq_host, kFallbackBlocks)),
+                       dim3(kMergeNT), 0, st, sl, (int32_t)k, maxflag, ix.doc_offset, ix.n_docs, ws,
+                       docs, scores);
+    return;
+  }
   // the fallback stage (query count on the device, usually 0): a few blocks
   const unsigned mgrid = (unsigned)(sg.nq_dev ? std::min<int64_t>(sg.nq_host, kFallbackBlocks)
                                               : sg.nq_host);

@@ -1,23 +1,46 @@
-"""Summarise rocprofv3 outputs under a gpurun_out dir: kernel stats + PMC
-counters per kernel (averaged per dispatch).  Dev tool."""
-import csv, glob, os, sys, collections
+"""Summarise rocprofv3 outputs of scripts/gpu_evidence.sh (PART=prof): the
+kernel stats of the bench run, then the PMC counters per workload tag and
+score phase (mean per dispatch) with derived per-row / traffic figures.
+Dev tool: python scripts/prof_summary.py gpurun_out/<NAME>"""
+import collections
+import csv
+import glob
+import os
+import re
+import sys
+
 d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 for f in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):
-    print("== kernel stats", f)
+    print("== kernel stats", os.path.relpath(f, d))
     for r in csv.DictReader(open(f)):
         name = r["Name"].split("(")[0].replace("void ", "").replace("bm25mi::", "")
-        print(f"  {name:38s} calls={int(r['Calls']):5d} avg={float(r['AverageNs'])/1e3:10.1f} us  pct={float(r['Percentage']):6.2f}")
+        print(f"  {name:44s} calls={int(r['Calls']):5d} avg={float(r['AverageNs'])/1e3:10.1f} us"
+              f"  pct={float(r['Percentage']):6.2f}")
+PH = {"0": "ALL", "1": "SAMPLE", "2": "REST"}
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-meta = {}
-for f in sorted(glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
-    tag = os.path.relpath(f, d).split(os.sep)[0]
+for f in sorted(glob.glob(os.path.join(d, "pmc_*", "**", "*counter_collection.csv"), recursive=True)):
+    tag = os.path.relpath(f, d).split(os.sep)[0].split("_")[1]
     for r in csv.DictReader(open(f)):
-        name = tag + ":" + r["Kernel_Name"].split("(")[0].replace("void ", "").replace("bm25mi::", "")
-        agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-        meta[name] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"], r["Workgroup_Size"])
-        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-        agg[name]["_dur_ns"].append(dur)
-for name, cs in agg.items():
-    print("== PMC", name, "vgpr/sgpr/lds/wg =", meta[name])
-    for c, v in sorted(cs.items()):
-        print(f"  {c:24s} {sum(v)/len(v):16.4g}  (n={len(v)})")
+        m = re.search(r"score_flat_kernel<(\d+), (\d), (\d), (\w+), (\d)>", r["Kernel_Name"])
+        key = (tag, PH[m.group(2)] + f" SM={m.group(3)} sparse={m.group(4)} TL={m.group(5)}") if m else (tag, r["Kernel_Name"][:40])
+        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        agg[key]["_dur_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+for (tag, ph), cs in sorted(agg.items()):
+    mean = {c: sum(v) / len(v) for c, v in cs.items()}
+    print(f"== PMC {tag} {ph}")
+    for c, v in sorted(mean.items()):
+        print(f"  {c:24s} {v:16.5g}")
+    if mean.get("SQ_INSTS_VMEM_RD", 0) > 0:
+        rows = mean["SQ_INSTS_VMEM_RD"] / 2
+        print(f"  -> rows {rows:.4g}; per row: VALU {mean.get('SQ_INSTS_VALU', 0) / rows:.1f} "
+              f"SALU {mean.get('SQ_INSTS_SALU', 0) / rows:.1f} LDS {mean.get('SQ_INSTS_LDS', 0) / rows:.2f}")
+    if mean.get("SQ_LDS_IDX_ACTIVE", 0) > 0 and "SQ_LDS_BANK_CONFLICT" in mean:
+        print(f"  -> LDS bank-conflict share {mean['SQ_LDS_BANK_CONFLICT'] / mean['SQ_LDS_IDX_ACTIVE']:.3f}")
+    if "TCC_EA0_RDREQ_sum" in mean:
+        h, m = mean.get("TCC_HIT_sum", 0), mean.get("TCC_MISS_sum", 0)
+        print(f"  -> EA read bytes {mean['TCC_EA0_RDREQ_sum'] * 128 / 1e9:.3f} GB (x128 B/req), "
+              f"DRAM-side {mean.get('TCC_EA0_RDREQ_DRAM_sum', 0) * 128 / 1e9:.3f} GB, L2 hit {h / max(h + m, 1):.3f}")
+    if mean.get("SQ_WAVE_CYCLES", 0) > 0:
+        w = mean["SQ_WAVE_CYCLES"]
+        print(f"  -> wave cycles: wait {mean.get('SQ_WAIT_ANY', 0) / w:.2f}, "
+              f"issue-stall {mean.get('SQ_WAIT_INST_ANY', 0) / w:.2f}, active {mean.get('SQ_ACTIVE_INST_ANY', 0) / w:.2f}")

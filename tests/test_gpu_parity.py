@@ -580,6 +580,22 @@ def test_sample_keys_per_tile_geometries(gpu):
         assert index.search_stats()["fallback_queries"] == 0
 
 
+def test_merge_paths_long_lists(gpu):
+    """The sampled main stage's merges: one wavefront per query for lists of
+    up to 2048 keys and k <= 1024 (merge_fast_kernel), the block merge for
+    longer lists (k = 600: ~8k keys above the sampled threshold) and larger
+    k (1500) — bit-exact either way."""
+    rng = np.random.default_rng(33)
+    N, V = 6_000_000, 300
+    ip, ix, dt = _rand_index(rng, N, V, 400_000)
+    q = rng.integers(-1, V, size=(24, 8)).astype(np.int32)
+    index = _idx(ip, ix, dt, N)
+    for k in (10, 250, 600, 1500):
+        _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
+        assert index.last_dispatch()["sample_p"] == _sample_p(index.info()["n_tiles"], k)
+        assert index.search_stats()["fallback_queries"] == 0
+
+
 def test_rare_queries_zero_fill_path(gpu):
     """Queries with fewer than k positive docs in the sample (rare terms) on a
     non-negative index: every positive doc + the smallest untouched ids —
