@@ -198,6 +198,8 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * kCounters), "hipMemset(counters)");
   HIP_TRY(hipMalloc(&ws.slow, sizeof(int32_t) * q), "hipMalloc(slow)");
   HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMalloc(wctr)");
+  // claim counters start at 0; each flat launch's last wave re-zeroes its region
+  HIP_TRY(hipMemset(ws.wctr, 0, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMemset(wctr)");
   ws.cap_seg = need_seg;
   if (ws.cap_seg > 0) HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * ws.cap_seg), "hipMalloc(seg)");
   ws.list_cap = C;

@@ -54,6 +54,8 @@ constexpr int kCtrStride = 64;
 // Sample tiles come in groups of kSampleGroup consecutive tiles (sample_geom).
 constexpr int kSampleGroup = 8;
 constexpr int kWctrInts = 8 * kClaimM * kCtrStride;
+// Finished-wave count of a claim counter's waves: 128 B past the counter.
+constexpr int kDoneOff = 32;
 // Claim-counter regions of a search: SAMPLE, REST (or the exact pass), fallback.
 constexpr int kWctrRegions = 3;
 

@@ -120,7 +120,7 @@ struct Stage {
   int32_t* fb;               // overflowed queries are appended here
   int32_t* fb_cnt;
   int32_t ctr_region;        // claim counters of the launch: ws.wctr + region * kWctrInts
-  bool ctr_zeroed;           // ... already zeroed by the search's zero_search_kernel
+                             // (zero at launch: each flat launch leaves its region zeroed)
   bool remap;                // merges: qmap gives the batch row of every array (the
                              // main stage's queries left to the block merge)
 };
@@ -738,7 +738,7 @@ struct FlatDesc {   // lane tile * 2^TL + term: the term's segment in the tile (
 // [lo, lo + n0), slot 1: lanes [0, n1) — and whether the row starts a tile
 // (and which tile of its item).
 constexpr uint32_t kRowNewTile = 1u << 17;
-constexpr uint32_t kRowNewItem = 1u << 24;   // the item's row 0 (a tile start unless the item is empty)
+constexpr uint32_t kRowParity = 1u << 24;    // the item's context slot (ctxV lanes 4 * parity ..)
 constexpr uint32_t kRowDead = 1u << 25;      // past the wave's last item
 __device__ __forceinline__ uint32_t row_lo(uint32_t w) { return w & 1u; }
 __device__ __forceinline__ uint32_t row_n0(uint32_t w) { return (w >> 1) & 0xFFu; }
@@ -758,12 +758,13 @@ struct FlatCtx {    // the item the accumulator's tile belongs to
 
 // Rows [j0, j0 + 64) of an item whose segment lane s holds segment
 // [sb, sb + sl), rows [excl, incl) of the item; prev = tile index of row
-// j0 - 1 (kNoTile at the item's first chunk: its first row starts a tile).
+// j0 - 1 (kNoTile at the item's first chunk: its first row starts a tile);
+// par = the item's context slot.
 constexpr uint32_t kNoTile = 0xFFFFFFFFu;
 template <int TL>
 __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t incl,
                                               uint32_t excl, uint32_t total, uint32_t j0,
-                                              uint32_t prev) {
+                                              uint32_t prev, uint32_t par) {
   const uint32_t lane = lane_id();
   const uint32_t j = j0 + lane;
   int pos = 0;  // segments ending at or before row j (binary lifting)
@@ -789,10 +790,7 @@ __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t
   const uint32_t tile = (uint32_t)pos >> TL;
   uint32_t tp = (uint32_t)__shfl_up((int)tile, 1, 64);
   if (lane == 0u) tp = prev;
-  // (an item with no rows at all still marks its row 0: the process side
-  // counts items to find their contexts)
-  t.w = masks | ((in && tile != tp) ? kRowNewTile : 0u) | (tile << 18) |
-        (j == 0u ? kRowNewItem : 0u);
+  t.w = masks | ((in && tile != tp) ? kRowNewTile : 0u) | (tile << 18) | (par ? kRowParity : 0u);
   t.last = lane_u32(tile, 63);
   return t;
 }
@@ -829,9 +827,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   const int grp = (int)(blockIdx.x & 7);
   const uint32_t lo = (uint32_t)(grp * per);
   const int32_t ngi = (int32_t)max<int64_t>(0, min<int64_t>(nitems, lo + per) - lo);
-  if (ngi == 0) return;  // wave-uniform; no barriers in this kernel
+  if (ngi == 0) return;  // wave-uniform; no barriers in this kernel (no claims made)
   const int32_t cm = (int32_t)(blockIdx.x >> 3) % claim_m;
   int32_t* ctr = wctr + (grp * kClaimM + cm) * kCtrStride;
+  // the last of the waves sharing a claim counter to finish resets it (and its
+  // finished count, on a line of its own) for the next launch on the region:
+  // no zeroing launch per search, and ~150 arrivals per count, not the grid's
+  auto finish = [&]() {
+    const int32_t g8 = (int32_t)(gridDim.x >> 3);
+    const int32_t sharers = g8 / claim_m + (cm < g8 % claim_m ? 1 : 0);
+    int32_t old = 0;
+    if (lane == 0) old = atomicAdd(ctr + kDoneOff, 1);
+    if (uniform(old) == sharers - 1 && lane == 0) {
+      ctr[0] = 0;
+      ctr[kDoneOff] = 0;
+    }
+  };
   const PostingRsrc pr = posting_rsrc(a);
   const uint32_t lt = lane & (TT - 1u), li = lane >> TL;  // segment lane: tile li, term lt
   const int64_t nbp = (a.ntiles + 7) >> 3;                // 8-tile groups of the sparse seg rows
@@ -923,8 +934,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // ---- the issue side's item: its segments (lane s = tile * TT + term) and
   // row numbering; the item prefetch pipeline one and two items ahead
   uint32_t iSb = 0, iSl = 0, iIncl = 0, iExcl = 0;
-  uint32_t iTotal = 0, iR = 0, iJ0 = 0, iPrev = kNoTile;
-  int32_t ctxV = 0, iPar = 0;
+  uint32_t iTotal = 0, iR = 0, iJ0 = 0, iPrev = kNoTile, iCur = 0;
+  int32_t ctxV = 0, iPar = 0;  // iPar: the context slot the next item takes
   FlatCur nx, nx2;
   FlatDesc dN;
   uint64_t thN = 0ull;
@@ -942,6 +953,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     // each tile): ALL, and REST without a positive threshold
     if ((PH == kAll || (PH == kRest && !th_pos)) && lt == 0u && (int)li < nx.bw)
       nr = max(nr, 1u);
+    if constexpr (PH == kSample) {
+      // a sample tile of the item without any posting row runs no epilogue:
+      // its keys are written here (0: no positive sum)
+      uint32_t tr = nr;
+#pragma unroll
+      for (int o = 1; o < (int)TT; o <<= 1) tr += (uint32_t)__shfl_xor((int)tr, o, 64);
+      if (lt == 0u && (int)li < nx.bw && tr == 0u) {
+        uint64_t* out = cand + (int64_t)nx.q * cstride + (int64_t)(nx.b * BW + (int32_t)li) * SM;
+#pragma unroll
+        for (int i = 0; i < SM; ++i) out[i] = 0ull;
+      }
+    }
     iIncl = scan64(nr);
     iExcl = iIncl - nr;
     iTotal = lane_u32(iIncl, 63);
@@ -958,6 +981,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       ctxV = c4 == 0 ? nx.q : c4 == 1 ? nx.b : c4 == 2 ? (int32_t)(uint32_t)thN
            : c4 == 3 ? (int32_t)(uint32_t)(thN >> 32) : ctxV;
     }
+    iCur = (uint32_t)iPar;
     iPar ^= 1;
     // prefetch: descriptors of the item after, terms of the one after that
     FlatCur nx3 = next(nx2);
@@ -974,7 +998,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   c0.b = c0.q = c0.qb = 0;
   c0.bw = 1;
   nx = next(c0);
-  if (nx.rit >= ngi) return;
+  if (nx.rit >= ngi) {
+    // (its claim returned: next() read it, so the count is final)
+    finish();
+    return;
+  }
   dN = load_bdesc(nx, terms_of(nx));
   thN = PH == kRest ? theta[nx.q] : 0ull;
   nx2 = next(nx);
@@ -1001,12 +1029,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       il = 0;
       return;
     }
-    tI = flat_chunk<TL>(iSb, iSl, iIncl, iExcl, iTotal, iJ0, iPrev);
+    tI = flat_chunk<TL>(iSb, iSl, iIncl, iExcl, iTotal, iJ0, iPrev, iCur);
     nI = min(64u, iR - iJ0);
     il = 0;
   };
   enter_item();
-  tI = flat_chunk<TL>(iSb, iSl, iIncl, iExcl, iTotal, 0u, iPrev);
+  tI = flat_chunk<TL>(iSb, iSl, iIncl, iExcl, iTotal, 0u, iPrev, iCur);
   nI = min(64u, iR);
   il = 0;
 
@@ -1027,7 +1055,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   for (int s = 0; s < kFR; ++s) issue(s);  // the first chunk holds >= kFR rows
 
   // process side
-  int32_t pPar = 1;  // parity of the process side's item (its first row flips it)
   FlatCtx ctxE{0, 0, 0ull};
   uint32_t curTi = kNoTile;  // the accumulator's tile (index in item ctxE), kNoTile: none
   // REST: the running maximum of the tile's sums (each doc's running sums
@@ -1081,12 +1108,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // s (consumed by the previous step), row r + 1 is prepared from slot s + 1
   auto step = [&](int s) {
     issue(s);
-    if (wC & (kRowNewTile | kRowNewItem)) {
-      if (wC & kRowNewItem) pPar ^= 1;
-    }
     if (wC & kRowNewTile) {
       if (curTi != kNoTile) epilogue();
       curTi = row_tile(wC) & kTileMask;
+      const int32_t pPar = (wC & kRowParity) ? 1 : 0;
       ctxE.q = __builtin_amdgcn_readlane(ctxV, 4 * pPar);
       ctxE.b = __builtin_amdgcn_readlane(ctxV, 4 * pPar + 1);
       ctxE.th = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(ctxV, 4 * pPar + 3) << 32) |
@@ -1108,6 +1133,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     for (int s = 0; s < kFR; ++s) step(s);
   }
   if (curTi != kNoTile) epilogue();
+  // every claim of this wave has returned (the last one, read by next(), ran
+  // out of items) before it counts itself finished
+  finish();
 }
 
 // ---------------------------------------------------------------------------
@@ -1472,7 +1500,13 @@ __global__ __launch_bounds__(256) void theta_wave_kernel(const uint64_t* __restr
                                                          int32_t k, uint64_t* __restrict__ theta,
                                                          int32_t* __restrict__ list_cnt,
                                                          int32_t C, int32_t nonneg,
-                                                         int64_t doc_offset, int64_t n_docs) {
+                                                         int64_t doc_offset, int64_t n_docs,
+                                                         int32_t* __restrict__ counters) {
+  // between the SAMPLE and the REST pass, this launch also resets what the
+  // rest of the search counts into (no zeroing launch per search): the list
+  // counts and the rescore / fallback / block-merge counters (the flat
+  // kernel's claim counters reset themselves)
+  if (blockIdx.x == 0 && threadIdx.x < kCounters) counters[threadIdx.x] = 0;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= Q) return;  // wave-uniform; no barriers
   const uint32_t lane = lane_id();
@@ -1547,7 +1581,7 @@ __global__ __launch_bounds__(256) void theta_wave_kernel(const uint64_t* __restr
         t = (t & ~0xFFFFFFFFull) | (uint64_t)(0xFFFFFFFFu - (uint32_t)min(L, n_docs));
     }
     theta[q] = t != 0ull ? t : (nonneg ? kZeroFillTheta : ~0ull);
-    if (t == 0ull && !nonneg) list_cnt[q] = C + 1;
+    list_cnt[q] = (t == 0ull && !nonneg) ? C + 1 : 0;
   }
 }
 
@@ -1958,7 +1992,6 @@ template <int S, int PH, int SM, int TL>
 static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t Qb,
                         const Stage& sg, const Workspace& ws, hipStream_t st) {
   int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;
-  if (!sg.ctr_zeroed) hipMemsetAsync(wctr, 0, sizeof(int32_t) * kWctrInts, st);
   // REST skips the sample tiles whose best key is below theta (m = 1 samples
   // in groups of 8 tiles: ws.cand holds this shard's sample keys)
   const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kSampleGroup;
@@ -2119,31 +2152,19 @@ static Stage fallback_stage(const DevIndex& ix, int64_t Q, const Workspace& ws) 
   return sg;
 }
 
-__global__ __launch_bounds__(256) void zero_search_kernel(uint64_t* __restrict__ keys, int64_t nk,
-                                                          int32_t* __restrict__ wctr, int64_t nw,
-                                                          int32_t* __restrict__ counters,
-                                                          int32_t* __restrict__ list_cnt, int64_t Q) {
-  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, st = (int64_t)gridDim.x * 256;
-  for (int64_t i = i0; i < nk; i += st) keys[i] = 0ull;
-  for (int64_t i = i0; i < nw; i += st) wctr[i] = 0;
-  for (int64_t i = i0; i < Q; i += st) list_cnt[i] = 0;
-  if (i0 < kCounters) counters[i0] = 0;
-}
-
 // SAMPLE pass: each query's S keys into keys[Q][S] (zero-padded); a copy
 // stays in ws.cand for the REST pass's sample-tile skip.
 template <int S_>
 static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
                      const SampleGeom& g, uint64_t* keys, const Workspace& ws, hipStream_t st) {
-  // one launch zeroes everything the search counts into: the sample keys, the
-  // claim counters of SAMPLE, REST and the fallback, the rescore/fallback
-  // counters and the list counts (each was a memset launch: ~5 us apiece)
-  hipLaunchKernelGGL(zero_search_kernel, dim3(64), dim3(256), 0, st, keys, Q * g.S, ws.wctr,
-                     (int64_t)kWctrRegions * kWctrInts, ws.counters, ws.list_cnt, Q);
+  // the SAMPLE pass writes a key (0: no positive sum) for every sample tile
+  // of every query; only a shard with fewer sample tiles than the widest
+  // shard leaves padding to clear.  Counters: theta_wave_kernel resets them.
+  if (sample_count(ix.ntiles, g.P, g.G) * g.m < g.S)
+    hipMemsetAsync(keys, 0, sizeof(uint64_t) * Q * g.S, st);
   if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, q, Q, T, ws, st);  // SAMPLE + REST + fallback
   Stage sg = main_stage(ix, Q, g.P, ws);
   sg.ctr_region = 0;
-  sg.ctr_zeroed = true;
   sg.M = g.m;
   sg.G = g.G;
   sg.cand_out = keys;
@@ -2164,19 +2185,17 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
     hipMemsetAsync(ws.counters, 0, kCounters * sizeof(int32_t), st);
     if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, q, Q, T, ws, st);
     sg.ctr_region = 2;
-    sg.ctr_zeroed = false;
     launch_phase<S_, kAll>(ix, q, T, Q, sg, ws, st);
     return;
   }
-  sg.ctr_region = 1;  // counters, list counts and claim counters: zeroed by sample_s
-  sg.ctr_zeroed = true;
+  sg.ctr_region = 1;  // counters and list counts: reset by theta_wave_kernel
   sg.M = g.m;
   sg.G = g.G;
   sg.sample_keys = ws.cand;  // launch_sample left this shard's keys there
   sg.sample_stride = g.S;
   hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, st, all_keys,
                      (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap,
-                     ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs);
+                     ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs, ws.counters);
   launch_phase<S_, kRest>(ix, q, T, Q, sg, ws, st);
 }
 
@@ -2257,11 +2276,10 @@ static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   if (P == 1) return;
   // queries whose list overflowed: exact pass over every tile (usually none;
   // the kernels read their count on the device and exit at once).  The
-  // rescore queue counters [0], [1] are still 0 from zero_search_kernel (the
+  // rescore queue counters [0], [1] are still 0 from theta_wave_kernel (the
   // sampled main stage has no tile candidates to rescore).
   Stage fb = fallback_stage(ix, Q, ws);
-  fb.ctr_region = 2;  // unused by the sampled search: zeroed by sample_s
-  fb.ctr_zeroed = true;
+  fb.ctr_region = 2;
   launch_phase<S_, kAll>(ix, q, T, Q, fb, ws, st);
   select_stage<S_>(ix, q, T, k, fb, ws, docs, scores, st);
 }
