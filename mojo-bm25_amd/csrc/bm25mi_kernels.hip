@@ -113,6 +113,7 @@ struct Stage {
   const int32_t* list_cnt;   // [nq]
   int32_t C;
   const uint64_t* sample_keys;  // REST: this shard's sample keys [nq][sample_stride] (null: none)
+  uint64_t* cand_mirror;        // SAMPLE (flat, m = 1): a second copy of cand_out's keys (or null)
   int64_t sample_stride;
   const int32_t* qmap;       // stage query -> batch row (null: identity)
   const int32_t* nq_dev;     // stage queries, on the device (null: nq_host)
@@ -605,7 +606,7 @@ __device__ __forceinline__ void best_dense(float* acc, int64_t tile, int64_t n_d
 // true>, about half its VALU work.
 template <int S>
 __device__ __forceinline__ void best1_pos(float* acc, int64_t tile, uint32_t idoff,
-                                          uint64_t* __restrict__ out) {
+                                          uint64_t* __restrict__ out, uint64_t* mirror) {
   constexpr int E4 = (1 << S) / 256;  // float4 groups per lane
   float4* a4 = reinterpret_cast<float4*>(acc);
   const uint32_t lane = lane_id();
@@ -634,6 +635,7 @@ __device__ __forceinline__ void best1_pos(float* acc, int64_t tile, uint32_t ido
   }
   zero_acc<S>(acc);
   if (lane == 0) *out = key;
+  if (lane == 1 && mirror) *mirror = key;
 }
 // ---------------------------------------------------------------------------
 // Persistent score kernel: kWaves independent waves per workgroup, each with a
@@ -807,7 +809,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int64_t cstride,
     uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
     int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
-    const uint64_t* __restrict__ skeys, int64_t sstride, int32_t BW) {
+    const uint64_t* __restrict__ skeys, int64_t sstride, int32_t BW, uint64_t* mirror) {
   constexpr int D = 1 << S;
   constexpr int kFR = PH == kSample ? BM25_FR_S : BM25_FR;  // ring slots (>= 2)
   constexpr uint32_t TT = 1u << TL;                          // term lanes per tile
@@ -963,6 +965,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
         uint64_t* out = cand + (int64_t)nx.q * cstride + (int64_t)(nx.b * BW + (int32_t)li) * SM;
 #pragma unroll
         for (int i = 0; i < SM; ++i) out[i] = 0ull;
+        if (SM == 1 && mirror) mirror[out - cand] = 0ull;
       }
     }
     iIncl = scan64(nr);
@@ -1079,7 +1082,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     } else {
       uint64_t* out = cand + (int64_t)ctxE.q * cstride + (int64_t)ti * SM;
       if constexpr (SM == 1)
-        best1_pos<S>(acc, tile, (uint32_t)a.doc_offset, out);
+        best1_pos<S>(acc, tile, (uint32_t)a.doc_offset, out, mirror ? mirror + (out - cand) : nullptr);
       else
         best_dense<S, SM, true>(acc, tile, a.n_docs, (uint32_t)a.doc_offset, out);
     }
@@ -1164,6 +1167,28 @@ __device__ __forceinline__ void bitonic_sort_desc(uint64_t* keys, int n) {
   }
 }
 
+// Exact top-k (k keys, zero-padded) of one tile of query q into out: wave 0
+// accumulates, the workgroup sorts the 2^S keys (acc: 2^S floats, keys: 2^S
+// u64, both LDS).
+template <int S>
+__device__ void rescore_tile(const IndexArgs& a, const int32_t* __restrict__ queries, int32_t T,
+                             int32_t k, int64_t q, int64_t tile, uint64_t* out, float* acc,
+                             uint64_t* keys) {
+  constexpr int D = 1 << S;
+  if (threadIdx.x < 64) {
+    zero_acc<S>(acc);
+    add_item<S>(a, tile, queries + q * T, T, acc);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += blockDim.x) {
+    const int64_t doc = (tile << S) + i;
+    keys[i] = doc < a.n_docs ? make_key(acc[i], (uint32_t)doc) : 0ull;
+  }
+  __syncthreads();
+  bitonic_sort_desc(keys, D);
+  for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = i < D ? keys[i] : 0ull;
+}
+
 template <int S>
 __global__ __launch_bounds__(kRescoreNT) void rescore_kernel(IndexArgs a,
                                                              const int32_t* __restrict__ queries,
@@ -1184,19 +1209,7 @@ __global__ __launch_bounds__(kRescoreNT) void rescore_kernel(IndexArgs a,
     const int64_t qi = code / maxflag;
     const int64_t q = sg.qmap ? (int64_t)sg.qmap[qi] : qi;
     const int64_t tile = sample_tile(ws.flag_tiles[code], sg.P, sg.G);
-    if (threadIdx.x < 64) {
-      zero_acc<S>(acc);
-      add_item<S>(a, tile, queries + q * T, T, acc);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < D; i += blockDim.x) {
-      const int64_t doc = (tile << S) + i;
-      keys[i] = doc < a.n_docs ? make_key(acc[i], (uint32_t)doc) : 0ull;
-    }
-    __syncthreads();
-    bitonic_sort_desc(keys, D);
-    uint64_t* out = ws.cand2 + (int64_t)code * k;
-    for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = i < D ? keys[i] : 0ull;
+    rescore_tile<S>(a, queries, T, k, q, tile, ws.cand2 + (int64_t)code * k, acc, keys);
   }
 }
 
@@ -1518,10 +1531,10 @@ __global__ __launch_bounds__(256) void theta_wave_kernel(const uint64_t* __restr
     if (n <= 64 * kThetaR) {
       uint64_t key[kThetaR];
 #pragma unroll
-      for (int j = 0; j < kThetaR; ++j) {
-        const int64_t i = (int64_t)j * 64 + lane;
-        const int64_t w = i / S;
-        key[j] = i < n ? all_keys[(w * Q + q) * S + (i - w * S)] : 0ull;
+      for (int j = 0; j < kThetaR; ++j) {  // (32-bit division: n <= 1024)
+        const uint32_t i = (uint32_t)j * 64u + lane;
+        const uint32_t w = i / (uint32_t)S;
+        key[j] = i < (uint32_t)n ? all_keys[((int64_t)w * Q + q) * S + (i - w * (uint32_t)S)] : 0ull;
       }
       // score half first (32 steps on u32), then the doc half among the keys
       // of that score — only when more than one key holds it (ties)
@@ -1690,31 +1703,17 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
 constexpr int kFastR = 32;      // list keys per lane held in registers
 constexpr int kFastMaxK = 1024; // largest k served (LDS: k keys per wave)
 
-__global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, int64_t doc_offset,
-                                                         Workspace ws, int32_t* __restrict__ docs,
-                                                         float* __restrict__ scores) {
-  __shared__ uint64_t sk[4][kFastMaxK];
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (q >= sg.nq_host) return;  // wave-uniform; no barriers in this kernel
+// The body of merge_fast_kernel for a list held in R keys per lane.
+template <int R>
+__device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64_t doc_offset,
+                                               int64_t q, int32_t cnt, uint64_t th,
+                                               uint64_t* keys, int32_t* __restrict__ docs,
+                                               float* __restrict__ scores) {
   const uint32_t lane = lane_id();
-  uint64_t* keys = sk[threadIdx.x >> 6];
-  const int32_t cnt = sg.list_cnt[q];
-  const uint64_t th = sg.theta[q];
-  if (cnt > sg.C) {  // overflowed: exact fallback stage
-    if (lane == 0) {
-      ws.nflag[q] = 0;
-      sg.fb[atomicAdd(sg.fb_cnt, 1)] = (int32_t)q;
-    }
-    return;
-  }
-  if (cnt > 64 * kFastR || (th == kZeroFillTheta && cnt < k)) {
-    if (lane == 0) ws.slow[atomicAdd(ws.counters + 4, 1)] = (int32_t)q;
-    return;
-  }
   const uint64_t* lst = sg.list + q * (int64_t)sg.C;
-  uint64_t key[kFastR];
+  uint64_t key[R];
 #pragma unroll
-  for (int j = 0; j < kFastR; ++j) {
+  for (int j = 0; j < R; ++j) {
     const int i = j * 64 + (int)lane;
     const uint64_t x = i < cnt ? lst[i] : 0ull;
     key[j] = x >= th ? x : 0ull;  // (every list key is >= theta; key 0 = empty)
@@ -1723,7 +1722,7 @@ __global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, in
   uint64_t kth = 0ull;
   uint32_t n = 0;
 #pragma unroll
-  for (int j = 0; j < kFastR; ++j) n += key[j] != 0ull;
+  for (int j = 0; j < R; ++j) n += key[j] != 0ull;
   n = wave_sum_u32(n);
   if (n > (uint32_t)k) {
     uint32_t need = (uint32_t)k, hi = 0u;
@@ -1731,7 +1730,7 @@ __global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, in
       const uint32_t hm = ~0u << bit, cand = hi | (1u << bit);
       uint32_t c = 0;
 #pragma unroll
-      for (int j = 0; j < kFastR; ++j) c += ((uint32_t)(key[j] >> 32) & hm) == cand;
+      for (int j = 0; j < R; ++j) c += ((uint32_t)(key[j] >> 32) & hm) == cand;
       const uint32_t tot = wave_sum_u32(c);
       if (tot >= need) hi = cand;
       else need -= tot;
@@ -1739,14 +1738,14 @@ __global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, in
     // need = rank of the answer among the keys of score hi
     uint32_t ties = 0;
 #pragma unroll
-    for (int j = 0; j < kFastR; ++j) ties += (uint32_t)(key[j] >> 32) == hi;
+    for (int j = 0; j < R; ++j) ties += (uint32_t)(key[j] >> 32) == hi;
     uint32_t lo = 0u;
     if (wave_sum_u32(ties) > 1u) {
       for (int bit = 31; bit >= 0; --bit) {
         const uint32_t hm = ~0u << bit, cand = lo | (1u << bit);
         uint32_t c = 0;
 #pragma unroll
-        for (int j = 0; j < kFastR; ++j)
+        for (int j = 0; j < R; ++j)
           c += ((uint32_t)(key[j] >> 32) == hi) & (((uint32_t)key[j] & hm) == cand);
         const uint32_t tot = wave_sum_u32(c);
         if (tot >= need) lo = cand;
@@ -1755,7 +1754,7 @@ __global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, in
     } else {
       uint32_t m = 0u;
 #pragma unroll
-      for (int j = 0; j < kFastR; ++j) m = (uint32_t)(key[j] >> 32) == hi ? (uint32_t)key[j] : m;
+      for (int j = 0; j < R; ++j) m = (uint32_t)(key[j] >> 32) == hi ? (uint32_t)key[j] : m;
       lo = wave_max_u32(m);
     }
     kth = ((uint64_t)hi << 32) | lo;
@@ -1765,7 +1764,7 @@ __global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, in
   const int m = next_pow2(n > 1u ? n : 2u);
   uint32_t base = 0u;
 #pragma unroll
-  for (int j = 0; j < kFastR; ++j) {
+  for (int j = 0; j < R; ++j) {
     const bool keep = key[j] != 0ull && key[j] >= kth;
     const uint64_t b = __ballot(keep);
     if (keep)
@@ -1802,6 +1801,39 @@ __global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, in
   }
 }
 
+__global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, int64_t doc_offset,
+                                                         Workspace ws, int32_t* __restrict__ docs,
+                                                         float* __restrict__ scores) {
+  __shared__ uint64_t sk[4][kFastMaxK];
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= sg.nq_host) return;  // wave-uniform; no barriers in this kernel
+  const uint32_t lane = lane_id();
+  uint64_t* keys = sk[threadIdx.x >> 6];
+  const int32_t cnt = sg.list_cnt[q];
+  const uint64_t th = sg.theta[q];
+  if (cnt > sg.C) {  // overflowed: exact fallback stage
+    if (lane == 0) {
+      ws.nflag[q] = 0;
+      sg.fb[atomicAdd(sg.fb_cnt, 1)] = (int32_t)q;
+    }
+    return;
+  }
+  if (cnt > 64 * kFastR || (th == kZeroFillTheta && cnt < k)) {
+    if (lane == 0) ws.slow[atomicAdd(ws.counters + 4, 1)] = (int32_t)q;
+    return;
+  }
+  // the fewest register slots that hold the list: 4, 8, 16 or 32 keys per lane
+  const int32_t nj = (cnt + 63) >> 6;
+  if (nj <= 4)
+    fast_merge_one<4>(sg, k, doc_offset, q, cnt, th, keys, docs, scores);
+  else if (nj <= 8)
+    fast_merge_one<8>(sg, k, doc_offset, q, cnt, th, keys, docs, scores);
+  else if (nj <= 16)
+    fast_merge_one<16>(sg, k, doc_offset, q, cnt, th, keys, docs, scores);
+  else
+    fast_merge_one<kFastR>(sg, k, doc_offset, q, cnt, th, keys, docs, scores);
+}
+
 __device__ void merge_final_one(const Stage& sg, int32_t k, int64_t maxflag, int64_t doc_offset,
                                 const Workspace& ws, int32_t* __restrict__ docs,
                                 float* __restrict__ scores, int64_t qi, uint64_t* keys,
@@ -1833,6 +1865,49 @@ __global__ __launch_bounds__(kMergeNT) void merge_final_kernel(
   for (int64_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
     __syncthreads();
     merge_final_one(sg, k, maxflag, doc_offset, ws, docs, scores, qi, keys, bits);
+  }
+}
+
+// The tail of a sampled search, one launch whose queries are counted on the
+// device (usually none): (1) the queries merge_fast_kernel left (lists longer
+// than it holds, zero-fill thresholds), merged as merge_first does; (2) the
+// fallback stage's queries (overflowed lists, re-scored over every tile by
+// the exact pass), each workgroup taking a whole query through merge_first,
+// the exact rescore of its flagged tiles and merge_final.  One launch in place
+// of four (each ~4.5 us even when it has nothing to do).
+template <int S>
+__global__ __launch_bounds__(kMergeNT) void merge_tail_kernel(
+    IndexArgs a, const int32_t* __restrict__ queries, int32_t T, Stage sl, Stage fb, int32_t k,
+    int64_t maxflag, Workspace ws, int32_t* __restrict__ docs, float* __restrict__ scores) {
+  __shared__ uint64_t keys[kMergeP];
+  __shared__ __attribute__((aligned(16))) float acc[1 << S];
+  __shared__ uint32_t bits[kMaxFlagBits / 32];
+  __shared__ int32_t s_nflag, s_cnt;
+  __shared__ uint32_t zf_bits[2 * kMaxK / 32];
+  static_assert((1 << S) <= kMergeP, "rescore keys live in the merge buffer");
+  const int64_t ns = stage_nq(sl);
+  for (int64_t i = blockIdx.x; i < ns; i += gridDim.x) {
+    __syncthreads();
+    merge_first_one(sl, k, maxflag, a.doc_offset, a.n_docs, ws, docs, scores,
+                    (int64_t)sl.qmap[i], keys, s_nflag, &s_cnt, zf_bits);
+  }
+  const int64_t nf = stage_nq(fb);
+  for (int64_t qi = blockIdx.x; qi < nf; qi += gridDim.x) {
+    __syncthreads();
+    merge_first_one(fb, k, maxflag, a.doc_offset, a.n_docs, ws, docs, scores, qi, keys, s_nflag,
+                    &s_cnt, zf_bits);
+    __syncthreads();
+    const int nfl = ws.nflag[qi];  // (written by thread 0 above)
+    if (nfl == 0) continue;
+    const int64_t q = (int64_t)fb.qmap[qi];
+    for (int i = 0; i < nfl; ++i) {
+      const int64_t code = qi * maxflag + i;
+      __syncthreads();
+      rescore_tile<S>(a, queries, T, k, q, (int64_t)ws.flag_tiles[code],
+                      ws.cand2 + code * k, acc, keys);
+    }
+    __syncthreads();
+    merge_final_one(fb, k, maxflag, a.doc_offset, ws, docs, scores, qi, keys, bits);
   }
 }
 
@@ -2009,7 +2084,8 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, st, a, q, (int32_t)T, sg.P,
                        sg.G, sg.nq_host, sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, sg.cstride,
                        ws.list, ws.list_cnt, ws.list_cap, wctr, ix.opt.claim_ch, ix.opt.claim_m,
-                       skip ? sg.sample_keys : nullptr, sg.sample_stride, bw);
+                       skip ? sg.sample_keys : nullptr, sg.sample_stride, bw,
+                       PH == kSample && SM == 1 ? sg.cand_mirror : nullptr);
   };
   if (ix.sparse)
     go(score_flat_kernel<S, PH, SM, true, TL>);
@@ -2152,8 +2228,9 @@ static Stage fallback_stage(const DevIndex& ix, int64_t Q, const Workspace& ws) 
   return sg;
 }
 
-// SAMPLE pass: each query's S keys into keys[Q][S] (zero-padded); a copy
-// stays in ws.cand for the REST pass's sample-tile skip.
+// SAMPLE pass: each query's S keys into keys[Q][S] (zero-padded); the flat
+// kernel also writes a copy (m = 1) into ws.cand for the REST pass's
+// sample-tile skip — the caller's buffer may change before launch_finish.
 template <int S_>
 static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
                      const SampleGeom& g, uint64_t* keys, const Workspace& ws, hipStream_t st) {
@@ -2168,10 +2245,9 @@ static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   sg.M = g.m;
   sg.G = g.G;
   sg.cand_out = keys;
+  sg.cand_mirror = keys != ws.cand ? ws.cand : nullptr;
   sg.cstride = g.S;
   launch_phase<S_, kSample>(ix, q, T, Q, sg, ws, st);
-  if (keys != ws.cand)
-    hipMemcpyAsync(ws.cand, keys, sizeof(uint64_t) * Q * g.S, hipMemcpyDeviceToDevice, st);
 }
 
 // theta from the W shards' sample keys [W][Q][S], then the REST pass (or, P =
@@ -2244,15 +2320,9 @@ static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k,
   if (sg.theta && !sg.qmap && sg.nt == 0 && k <= kFastMaxK) {
     // sampled main stage: one wavefront per query; the queries it leaves go
     // to the block merge below (their count on the device, usually 0)
+    // (merge_tail_kernel takes the queries it leaves)
     hipLaunchKernelGGL(merge_fast_kernel, dim3((unsigned)((sg.nq_host + 3) / 4)), dim3(256), 0,
                        st, sg, (int32_t)k, ix.doc_offset, ws, docs, scores);
-    Stage sl = sg;
-    sl.qmap = ws.slow;
-    sl.nq_dev = ws.counters + 4;
-    sl.remap = true;
-    hipLaunchKernelGGL(merge_first_kernel, dim3((unsigned)std::min<int64_t>(sg.nq_host, kFallbackBlocks)),
-                       dim3(kMergeNT), 0, st, sl, (int32_t)k, maxflag, ix.doc_offset, ix.n_docs, ws,
-                       docs, scores);
     return;
   }
   // the fallback stage (query count on the device, usually 0): a few blocks
@@ -2272,7 +2342,8 @@ static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k,
 template <int S_>
 static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k, int P,
                      const Workspace& ws, int32_t* docs, float* scores, hipStream_t st) {
-  select_stage<S_>(ix, q, T, k, main_stage(ix, Q, P, ws), ws, docs, scores, st);
+  const Stage ms = main_stage(ix, Q, P, ws);
+  select_stage<S_>(ix, q, T, k, ms, ws, docs, scores, st);
   if (P == 1) return;
   // queries whose list overflowed: exact pass over every tile (usually none;
   // the kernels read their count on the device and exit at once).  The
@@ -2281,7 +2352,17 @@ static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   Stage fb = fallback_stage(ix, Q, ws);
   fb.ctr_region = 2;
   launch_phase<S_, kAll>(ix, q, T, Q, fb, ws, st);
-  select_stage<S_>(ix, q, T, k, fb, ws, docs, scores, st);
+  if (k > kFastMaxK) {  // the block merges throughout
+    select_stage<S_>(ix, q, T, k, fb, ws, docs, scores, st);
+    return;
+  }
+  Stage sl = ms;  // the queries merge_fast_kernel left
+  sl.qmap = ws.slow;
+  sl.nq_dev = ws.counters + 4;
+  sl.remap = true;
+  hipLaunchKernelGGL(merge_tail_kernel<S_>, dim3((unsigned)std::min<int64_t>(Q, kFallbackBlocks)),
+                     dim3(kMergeNT), 0, st, args_of(ix), q, (int32_t)T, sl, fb, (int32_t)k,
+                     maxflag_for(k, fb.nt), ws, docs, scores);
 }
 
 hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
