@@ -1048,12 +1048,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     if (il == nI) next_chunk();
     const uint32_t base = lane_u32(tI.base, (int)il);
     wR[s] = lane_u32(tI.w, (int)il);
-    ldR[s] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)(lane * 4u), (int)(base * 2u), 0);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)(lane * 8u), (int)(base * 4u), 0);
+#if BM25_MASKLD == 1
+    // lanes past the row's last valid pair issue no load (the slot keeps an
+    // older row's finite values; the row word masks them)
+    if (lane < row_lo(wR[s]) + row_n0(wR[s])) {
+#endif
+#if BM25_MASKLD == 2
+    // lanes past the row's last valid pair re-read lane 0's pair (a line the
+    // row fetches anyway): a row touches only its segment's lines
+    const bool lv = lane < row_lo(wR[s]) + row_n0(wR[s]);
+    const uint32_t lo4 = lv ? lane * 4u : 0u, lo8 = lv ? lane * 8u : 0u;
+#else
+    const uint32_t lo4 = lane * 4u, lo8 = lane * 8u;
+#endif
+    ldR[s] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)lo4, (int)(base * 2u), 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)lo8, (int)(base * 4u), 0);
     v0R[s] = __uint_as_float((uint32_t)v[0]);
     v1R[s] = __uint_as_float((uint32_t)v[1]);
+#if BM25_MASKLD == 1
+    }
+#endif
     ++il;
   };
+#if BM25_MASKLD == 1
+#pragma unroll
+  for (int s = 0; s < kFR; ++s) ldR[s] = 0u, v0R[s] = v1R[s] = 0.f;
+#endif
 #pragma unroll
   for (int s = 0; s < kFR; ++s) issue(s);  // the first chunk holds >= kFR rows
 
