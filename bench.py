@@ -71,11 +71,13 @@ def load_traffic(path: str, config: str, shift: int, terms: int):
     try:
         with open(path) as f:
             t = json.load(f)
-        if (t.get("config") == config and int(t.get("tile_shift", -1)) == shift
-                and int(t.get("terms_per_query", 8)) == terms):
-            return t
     except (OSError, ValueError):
-        pass
+        return None
+    for e in t.get("entries", [t]):
+        if (e.get("config") == config and int(e.get("tile_shift", -1)) == shift
+                and int(e.get("terms_per_query", 8)) == terms):
+            return dict(e, method=t.get("method", e.get("method")),
+                        source=t.get("source", e.get("source")))
     return None
 
 
@@ -323,8 +325,9 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-                "traffic_source": (f"profiles/traffic.json: {traffic.get('method')}; "
-                                   f"L2 hit rate {traffic.get('l2_hit_rate')}") if traffic else None,
+                "traffic_source": (f"profiles/traffic.json ({traffic.get('source')}): "
+                                   f"{traffic.get('method')}; L2 hit rate "
+                                   f"{traffic.get('l2_hit_rate')}") if traffic else None,
                 "kernel": "score pass (score_flat_kernel SAMPLE + theta_wave_kernel + "
                           "score_flat_kernel REST)",
                 "kernel_ms": round(kern_ms, 4),

@@ -273,8 +273,27 @@ __device__ __forceinline__ void add_item(const IndexArgs& a, int64_t tile,
   }
 }
 
+#define BM25_ZA(o) "ds_write_addtid_b32 %1 offset:" #o "\n"
 template <int S>
 __device__ __forceinline__ void zero_acc(float* acc) {
+  if constexpr (S == 11) {
+    // ds_write_addtid_b32 stores lane l at M0 + offset + 4 l: no address VGPR
+    // to move, 2 cycles per 256 B (128 B/clk/CU, vs ~79 for ds_write_b128);
+    // clearing the tile is a large part of the flat kernel's LDS time
+    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)acc;
+    // (an M0 write needs a wait state before an instruction reads M0)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n"
+                 BM25_ZA(0) BM25_ZA(256) BM25_ZA(512) BM25_ZA(768) BM25_ZA(1024) BM25_ZA(1280)
+                 BM25_ZA(1536) BM25_ZA(1792) BM25_ZA(2048) BM25_ZA(2304) BM25_ZA(2560) BM25_ZA(2816)
+                 BM25_ZA(3072) BM25_ZA(3328) BM25_ZA(3584) BM25_ZA(3840) BM25_ZA(4096) BM25_ZA(4352)
+                 BM25_ZA(4608) BM25_ZA(4864) BM25_ZA(5120) BM25_ZA(5376) BM25_ZA(5632) BM25_ZA(5888)
+                 BM25_ZA(6144) BM25_ZA(6400) BM25_ZA(6656) BM25_ZA(6912) BM25_ZA(7168) BM25_ZA(7424)
+                 BM25_ZA(7680) BM25_ZA(7936)
+                 :
+                 : "s"(la), "v"(0.f)
+                 : "memory", "m0");
+    return;
+  }
   float4* a4 = reinterpret_cast<float4*>(acc);
 #pragma unroll
   for (int j = 0; j < (1 << S) / 256; ++j) a4[j * 64 + lane_id()] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1048,32 +1067,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     if (il == nI) next_chunk();
     const uint32_t base = lane_u32(tI.base, (int)il);
     wR[s] = lane_u32(tI.w, (int)il);
-#if BM25_MASKLD == 1
-    // lanes past the row's last valid pair issue no load (the slot keeps an
-    // older row's finite values; the row word masks them)
-    if (lane < row_lo(wR[s]) + row_n0(wR[s])) {
-#endif
-#if BM25_MASKLD == 2
-    // lanes past the row's last valid pair re-read lane 0's pair (a line the
-    // row fetches anyway): a row touches only its segment's lines
-    const bool lv = lane < row_lo(wR[s]) + row_n0(wR[s]);
-    const uint32_t lo4 = lv ? lane * 4u : 0u, lo8 = lv ? lane * 8u : 0u;
-#else
     const uint32_t lo4 = lane * 4u, lo8 = lane * 8u;
-#endif
     ldR[s] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)lo4, (int)(base * 2u), 0);
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)lo8, (int)(base * 4u), 0);
     v0R[s] = __uint_as_float((uint32_t)v[0]);
     v1R[s] = __uint_as_float((uint32_t)v[1]);
-#if BM25_MASKLD == 1
-    }
-#endif
     ++il;
   };
-#if BM25_MASKLD == 1
-#pragma unroll
-  for (int s = 0; s < kFR; ++s) ldR[s] = 0u, v0R[s] = v1R[s] = 0.f;
-#endif
 #pragma unroll
   for (int s = 0; s < kFR; ++s) issue(s);  // the first chunk holds >= kFR rows
 

@@ -1,7 +1,10 @@
 """Summarise rocprofv3 outputs of scripts/gpu_evidence.sh (PART=prof): the
 kernel stats of the bench run, then the PMC counters per workload tag and
 score phase (mean per dispatch) with derived per-row / traffic figures.
-Dev tool: python scripts/prof_summary.py gpurun_out/<NAME>"""
+With --traffic OUT.json, also write the per-workload HBM traffic of one
+search (EA read requests x 128 B + WRITE_SIZE, summed over the score
+phases) that bench.py reports as roofline.traffic.
+Dev tool: python scripts/prof_summary.py gpurun_out/<NAME> [--traffic profiles/traffic.json]"""
 import collections
 import csv
 import glob
@@ -9,7 +12,13 @@ import os
 import re
 import sys
 
-d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+import json
+
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+d = args[0] if args else "gpurun_out"
+traffic_out = sys.argv[sys.argv.index("--traffic") + 1] if "--traffic" in sys.argv else None
+if traffic_out in args:
+    args.remove(traffic_out)
 for f in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):
     print("== kernel stats", os.path.relpath(f, d))
     for r in csv.DictReader(open(f)):
@@ -44,3 +53,29 @@ for (tag, ph), cs in sorted(agg.items()):
         w = mean["SQ_WAVE_CYCLES"]
         print(f"  -> wave cycles: wait {mean.get('SQ_WAIT_ANY', 0) / w:.2f}, "
               f"issue-stall {mean.get('SQ_WAIT_INST_ANY', 0) / w:.2f}, active {mean.get('SQ_ACTIVE_INST_ANY', 0) / w:.2f}")
+
+# per-workload traffic of one search (each phase is one dispatch per search)
+WL = {"c3": ("c3", 8), "t16": ("c3", 16), "c5": ("c5", 8)}
+if traffic_out:
+    entries = []
+    for tag, (config, terms) in WL.items():
+        ph = {p: {c: sum(v) / len(v) for c, v in cs.items()} for (t, p), cs in agg.items() if t == tag}
+        if not ph:
+            continue
+        rd = sum(m.get("TCC_EA0_RDREQ_sum", 0) for m in ph.values())
+        wr = sum(m.get("WRITE_SIZE", 0) for m in ph.values()) * 1024
+        hit = sum(m.get("TCC_HIT_sum", 0) for m in ph.values())
+        miss = sum(m.get("TCC_MISS_sum", 0) for m in ph.values())
+        entries.append({"config": config, "terms_per_query": terms, "tile_shift": 11,
+                        "hbm_bytes_per_launch": int(rd * 128 + wr), "read_bytes": int(rd * 128),
+                        "write_size_bytes": int(wr), "tcc_ea0_rdreq": int(rd),
+                        "l2_hit_rate": round(hit / max(hit + miss, 1), 3),
+                        "phases": sorted(ph)})
+    json.dump({"source": os.path.relpath(d), "kernels": "score_flat_kernel ALL + SAMPLE + REST (one search)",
+               "method": ("rocprofv3 --pmc, one counter group per pass (scripts/gpu_evidence.sh PART=prof); "
+                          "read bytes = TCC_EA0_RDREQ x 128 B, the bytes per request measured for this "
+                          "kernel's 4-B and 8-B-per-lane buffer loads by the calibration kernel "
+                          "(profiles/r02/traffic_calib/summary.json: 128.0 B/RDREQ, FETCH_SIZE reports "
+                          "half); + WRITE_SIZE (KB); Infinity-Cache hits are included (not separable)"),
+               "entries": entries}, open(traffic_out, "w"), indent=1)
+    print("wrote", traffic_out, [(e["config"], e["terms_per_query"], e["hbm_bytes_per_launch"]) for e in entries])
