@@ -1080,9 +1080,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // process side
   FlatCtx ctxE{0, 0, 0ull};
   uint32_t curTi = kNoTile;  // the accumulator's tile (index in item ctxE), kNoTile: none
-  // REST: the running maximum of the tile's sums (each doc's running sums
-  // only grow on a non-negative index, so the tile holds a key >= theta only
-  // if this reaches theta's score)
+  // REST and SAMPLE: the running maximum of the tile's sums (each doc's
+  // running sums only grow on a non-negative index, so it is the tile's best
+  // sum; REST: the tile holds a key >= theta only if this reaches theta's score)
   float hmax = 0.f;
   bool done = false;
 
@@ -1101,9 +1101,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + (int64_t)ctxE.q * cstride + tile * kTileM);
     } else {
       uint64_t* out = cand + (int64_t)ctxE.q * cstride + (int64_t)ti * SM;
-      if constexpr (SM == 1)
-        best1_pos<S>(acc, tile, (uint32_t)a.doc_offset, out, mirror ? mirror + (out - cand) : nullptr);
-      else
+      if constexpr (SM == 1) {
+        if (a.nonneg) {
+          // running sums only grow on a non-negative index: the tile's best
+          // sum is the running maximum, no pass over the accumulator.  Its
+          // key takes the tile's last doc (a key <= the best doc's own), so
+          // k real keys still reach theta
+          const uint32_t wm = wave_max_u32(__float_as_uint(hmax));
+          const uint32_t last = (uint32_t)min<int64_t>((tile << S) + D - 1, a.n_docs - 1);
+          const uint64_t key = wm == 0u ? 0ull
+                               : ((uint64_t)score_key(__uint_as_float(wm)) << 32) |
+                                     (uint64_t)(0xFFFFFFFFu - last - (uint32_t)a.doc_offset);
+          zero_acc<S>(acc);
+          if (lane == 0) *out = key;
+          if (lane == 1 && mirror) mirror[out - cand] = key;
+          hmax = 0.f;
+        } else {
+          best1_pos<S>(acc, tile, (uint32_t)a.doc_offset, out, mirror ? mirror + (out - cand) : nullptr);
+        }
+      } else
         best_dense<S, SM, true>(acc, tile, a.n_docs, (uint32_t)a.doc_offset, out);
     }
   };
@@ -1146,7 +1162,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const float y0 = xc0 + ac0, y1 = xc1 + ac1;
     lds_at(sc0) = y0;
     lds_at(sc1) = y1;
-    if (PH == kRest) hmax = fmaxf(hmax, fmaxf(y0, y1));
+    if (PH == kRest || (PH == kSample && SM == 1)) hmax = fmaxf(hmax, fmaxf(y0, y1));
     done = (wC & kRowDead) != 0u;  // (rows past the last item add nothing)
     prepare((s + 1) % kFR);
   };
