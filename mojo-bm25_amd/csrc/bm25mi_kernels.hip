@@ -767,7 +767,7 @@ __device__ __forceinline__ uint32_t row_n1(uint32_t w) { return (w >> 9) & 0xFFu
 __device__ __forceinline__ uint32_t row_tile(uint32_t w) { return (w >> 18) & 0x3Fu; }
 
 struct FlatTab {    // one chunk of an item's rows: lane r = row j0 + r
-  uint32_t base;    // even posting index of the row's first pair (0: dead row)
+  uint32_t base;    // ldoc byte offset of the row's first pair (2 x an even posting index; 0: dead row)
   uint32_t w;       // row word (above); 0: padding row
   uint32_t last;    // (uniform) tile index of the chunk's row 63 (the next chunk's predecessor)
 };
@@ -800,7 +800,7 @@ __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t
   const bool in = j < total;
   FlatTab t;
   const uint32_t k = j - e;  // row of its segment
-  t.base = (in && l != 0u) ? (b & ~1u) + 128u * k : 0u;
+  t.base = (in && l != 0u) ? ((b & ~1u) + 128u * k) * 2u : 0u;
   // row positions p of the segment: p + base in [b, b + l)
   const uint32_t rlo = k == 0u ? (b & 1u) : 0u;
   const uint32_t rhi = min(128u, (b & 1u) + l - 128u * k);
@@ -1068,8 +1068,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const uint32_t base = lane_u32(tI.base, (int)il);
     wR[s] = lane_u32(tI.w, (int)il);
     const uint32_t lo4 = lane * 4u, lo8 = lane * 8u;
-    ldR[s] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)lo4, (int)(base * 2u), 0);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)lo8, (int)(base * 4u), 0);
+    ldR[s] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)lo4, (int)base, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)lo8, (int)(base * 2u), 0);
     v0R[s] = __uint_as_float((uint32_t)v[0]);
     v1R[s] = __uint_as_float((uint32_t)v[1]);
     ++il;
