@@ -505,8 +505,6 @@ __device__ __forceinline__ void emit_rest(float* acc, int64_t tile, int64_t n_do
 #pragma unroll 1
   for (int j0 = 0; j0 < D / 256; j0 += 2) {  // not unrolled: 8 entries live at a time
     const float4 f0 = a4[j0 * 64 + lane], f1 = a4[(j0 + 1) * 64 + lane];
-    a4[j0 * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-    a4[(j0 + 1) * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     const float fe[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
     const float mx = fmaxf(fmaxf(fmaxf(fe[0], fe[1]), fmaxf(fe[2], fe[3])),
                            fmaxf(fmaxf(fe[4], fe[5]), fmaxf(fe[6], fe[7])));
@@ -535,6 +533,7 @@ __device__ __forceinline__ void emit_rest(float* acc, int64_t tile, int64_t n_do
       }
     }
   }
+  zero_acc<S>(acc);  // (LDS order: after every read above)
 }
 
 // Tiles of a phase: SAMPLE visits the sample tiles (sample_tile), ALL and
