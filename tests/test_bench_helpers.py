@@ -1,0 +1,48 @@
+"""bench.py's host-side helpers (no GPU): the per-workload PMC traffic lookup
+behind roofline.traffic and the SURVEY.md §8(d) algorithmic byte count
+behind roofline.achieved."""
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def test_traffic_entries_match_their_workload():
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    seen = {}
+    for config, terms in (("c3", 8), ("c3", 16), ("c5", 8)):
+        t = bench.load_traffic(path, config, 11, terms)
+        assert t is not None, (config, terms)
+        assert t["config"] == config and t["terms_per_query"] == terms
+        assert abs(t["hbm_bytes_per_launch"] - t["read_bytes"] - t["write_size_bytes"]) <= 2
+        assert t["hbm_bytes_per_launch"] > 0
+        assert 0.0 < t["l2_hit_rate"] < 1.0 and t["method"] and t["source"]
+        seen[(config, terms)] = t["hbm_bytes_per_launch"]
+    # 16-term queries read about twice the postings of 8-term ones
+    assert seen[("c3", 16)] > 1.5 * seen[("c3", 8)]
+    assert bench.load_traffic(path, "c3", 12, 8) is None  # other tile size
+    assert bench.load_traffic(path, "c2", 11, 8) is None  # never profiled
+
+
+def test_traffic_single_entry_file(tmp_path):
+    """The round-2 layout (one workload at the top level) still loads."""
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps({"config": "c3", "tile_shift": 11, "hbm_bytes_per_launch": 5,
+                             "method": "m"}))
+    assert bench.load_traffic(str(p), "c3", 11, 8)["hbm_bytes_per_launch"] == 5
+    assert bench.load_traffic(str(p), "c3", 11, 16) is None
+    assert bench.load_traffic(str(tmp_path / "missing.json"), "c3", 11, 8) is None
+
+
+def test_algorithmic_bytes_formula():
+    # terms 0..3 with df 2, 0, 5, 1; padding and a repeated term count once
+    indptr = np.array([0, 2, 2, 7, 8], np.int64)
+    q = np.array([[0, 2, 2, -1], [3, -1, -1, -1]], np.int32)
+    k = 10
+    want = ((8 * 2 + 8) + (8 * 5 + 8) + 4 * 4 + 8 * k) + ((8 * 1 + 8) + 4 * 4 + 8 * k)
+    assert bench.algorithmic_bytes(indptr, q, k) == want
