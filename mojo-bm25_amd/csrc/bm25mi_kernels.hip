@@ -273,7 +273,7 @@ __device__ __forceinline__ void add_item(const IndexArgs& a, int64_t tile,
   }
 }
 
-#define BM25_ZA(o) "ds_write_addtid_b32 %1 offset:" #o "\n"
+#define BM25_ZA(o) "ds_write_addtid_b32 %2 offset:" #o "\n"
 template <int S>
 __device__ __forceinline__ void zero_acc(float* acc) {
   if constexpr (S == 11) {
@@ -281,17 +281,21 @@ __device__ __forceinline__ void zero_acc(float* acc) {
     // to move, 2 cycles per 256 B (128 B/clk/CU, vs ~79 for ds_write_b128);
     // clearing the tile is a large part of the flat kernel's LDS time
     const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)acc;
-    // (an M0 write needs a wait state before an instruction reads M0)
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n"
+    // M0 is the compiler's (it sets it for its own lane-select uses): saved
+    // and restored here.  An M0 write needs a wait state before an
+    // instruction reads M0 (without it the first store used a stale M0).
+    uint32_t m0_saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 1\n"
                  BM25_ZA(0) BM25_ZA(256) BM25_ZA(512) BM25_ZA(768) BM25_ZA(1024) BM25_ZA(1280)
                  BM25_ZA(1536) BM25_ZA(1792) BM25_ZA(2048) BM25_ZA(2304) BM25_ZA(2560) BM25_ZA(2816)
                  BM25_ZA(3072) BM25_ZA(3328) BM25_ZA(3584) BM25_ZA(3840) BM25_ZA(4096) BM25_ZA(4352)
                  BM25_ZA(4608) BM25_ZA(4864) BM25_ZA(5120) BM25_ZA(5376) BM25_ZA(5632) BM25_ZA(5888)
                  BM25_ZA(6144) BM25_ZA(6400) BM25_ZA(6656) BM25_ZA(6912) BM25_ZA(7168) BM25_ZA(7424)
                  BM25_ZA(7680) BM25_ZA(7936)
-                 :
+                 "s_mov_b32 m0, %0\n\ts_nop 1"
+                 : "=&s"(m0_saved)
                  : "s"(la), "v"(0.f)
-                 : "memory", "m0");
+                 : "memory");
     return;
   }
   float4* a4 = reinterpret_cast<float4*>(acc);
