@@ -100,6 +100,8 @@ int bm25_index_segments(const bm25_index* idx, int32_t* sparse, int64_t* n_pairs
  *   queries    [Q, T] int32, negative = padding, every id < n_terms
  *   out_docs   [Q, k] int32
  *   out_scores [Q, k] f32
+ * Every 0 <= k <= n_docs is served (k > 4096 by the exact large-k path:
+ * dense scores, radix selection of the k-th key, sort of the k survivors).
  * Errors: EINVAL when a token id >= n_terms (message matches
  * bm25_native.py:118-121), when k < 0 or k > n_docs.
  */
@@ -196,7 +198,8 @@ int bm25_merge_sorted_device(int device, const int32_t* d_docs,
  * the same query batch in two halves around one all-gather:
  *   bm25_sample_width(idx, shard_docs_max, world, k, &S): keys per query each
  *     rank samples (the same on every rank: shard_docs_max = the largest
- *     shard's document count; S = 0: shards too small to sample);
+ *     shard's document count; S = 0: shards too small to sample, or
+ *     k > 4096 — then the finish half lists the shard's exact top-k);
  *   bm25_search_sample_device(...): this shard's sample keys -> d_keys
  *     (u64 [Q][S], zero-padded);
  *   (caller) all-gather d_keys of every rank -> d_all_keys [world][Q][S];

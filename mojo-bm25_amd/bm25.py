@@ -15,10 +15,9 @@ columns with numpy; scores agree to ~1e-7 relative (north_star tolerance
 1e-4) and are returned as float64 arrays like the reference's.  Documents with
 equal scores are ranked by index ascending (the reference's
 ``argsort(...)[::-1]`` order among ties is implementation-defined).
-``get_top_n`` with n <= 4096 (kMaxK) runs the engine's batched top-k; above
-it (the reference, bm25.py:172-178, ranks every document) the GPU's dense
-per-document scores are ranked by (score desc, index asc) — the ordering of
-an output vector, as the reference's own argsort.
+``get_top_n`` runs the engine's batched top-k for every n (above 4096 the
+exact large-k path, bm25mi_large.hip; the reference, bm25.py:172-178, ranks
+every document).
 """
 from __future__ import annotations
 
@@ -30,9 +29,6 @@ import scipy.sparse as sp
 
 from bm25mi.index import GpuIndex
 from bm25mi.scoring import build_scores
-
-MAX_TOP_K = 4096  # kMaxK of libbm25mi (bm25mi_internal.h)
-
 
 class BM25:
     """BM25 with a precomputed dense score matrix, scored on the GPU."""
@@ -137,12 +133,6 @@ class BM25:
             return []
         num = min(n, self.corpus_size)
         ids = self._query_ids(query)
-        if num > MAX_TOP_K:
-            # past the engine's top-k limit: rank the GPU's dense scores
-            # (bm25.py:172-178 argsorts every score)
-            scores = self.get_scores(query).astype(np.float32)
-            order = np.lexsort((np.arange(self.corpus_size), -scores))[:num]
-            return [(np.float64(scores[d]), corpus[int(d)]) for d in order]
         q = np.full((1, max(len(ids), 1)), -1, np.int32)
         q[0, :len(ids)] = ids
         docs, scores = self._gpu.search(q, num)

@@ -10,8 +10,10 @@ Deliberate differences:
   * invalid query arrays raise ValueError directly (the reference first drops
     into ``breakpoint()``, bm25_native.py:113);
   * documents with equal scores are ordered by doc id ascending (the
-    reference's order is numpy-implementation-defined, bm25_native.py:205-212);
-  * top_k is limited to 4096 (kMaxK) — larger k raises ValueError.
+    reference's order is numpy-implementation-defined, bm25_native.py:205-212).
+Every top_k <= num_docs is served, as by the reference's argpartition
+(bm25_native.py:204-214): k <= 4096 by the sampled-threshold pipeline, larger
+k by the exact dense-score radix selection (csrc/bm25mi_large.hip).
 """
 from __future__ import annotations
 

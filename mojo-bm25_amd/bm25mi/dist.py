@@ -73,10 +73,15 @@ def gpu_merge(device: int, stream=None) -> MergeFn:
     return merge
 
 
+def _group_key(group):
+    return dist.group.WORLD if group is None else group
+
+
 def _global_docs(index, device, group=None) -> int:
     """Documents of the whole collection: the sum of every rank's shard,
-    all-reduced once and cached on the index object."""
-    n = getattr(index, "_bm25_global_docs", None)
+    all-reduced once per process group and cached on the index object."""
+    cache = index.__dict__.setdefault("_bm25_global_docs", {})
+    n = cache.get(_group_key(group))
     if n is None:
         if dist.get_world_size(group) == 1:
             n = int(index.n_docs)
@@ -86,8 +91,28 @@ def _global_docs(index, device, group=None) -> int:
                              device="cpu" if backend == "gloo" else device)
             dist.all_reduce(t, group=group)
             n = int(t.item())
-        index._bm25_global_docs = n
+        cache[_group_key(group)] = n
     return n
+
+
+def _agree_width(index, S: int, k: int, device, group=None) -> None:
+    """Every rank must sample the same width S (the key all-gather has one
+    shape): it depends on k, the world and the handle's ``sample_p`` option,
+    which each rank sets on its own.  Checked once per (group, k) by one
+    all-reduce of (S, -S) with MAX; every rank raises the same ValueError when
+    they differ."""
+    seen = index.__dict__.setdefault("_bm25_width_ok", set())
+    key = (_group_key(group), int(k))
+    if key in seen:
+        return
+    backend = dist.get_backend(group)
+    t = torch.tensor([S, -S], dtype=torch.int64, device="cpu" if backend == "gloo" else device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    lo, hi = -int(t[1].item()), int(t[0].item())
+    if lo != hi:
+        raise ValueError(f"ranks disagree on the sample width at k={k} (min {lo}, max {hi}): "
+                         "set the same sample_p option on every rank's index")
+    seen.add(key)
 
 
 def gather_keys(keys: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
@@ -121,21 +146,22 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
     single-index search checks it (numpy's argpartition error,
     bm25_native.py:205): ``n_docs_total``, or one all-reduce of the shards'
     counts on the first search (cached on ``index``)."""
+    world = int(exchange.world) if exchange is not None else dist.get_world_size(group)
+    total = n_docs_total if n_docs_total is not None else (
+        _global_docs(index, d_queries.device, group) if exchange is None else None)
+    if total is not None and k > total:
+        raise ValueError(f"kth(={total - k}) out of bounds ({total})")
+    # (k > 4096: S = 0, every shard's exact top-k — bm25mi_large.hip)
+    S = index.sample_width(k, world, shard_docs_max)
+    if exchange is None and world > 1:
+        _agree_width(index, S, k, d_queries.device, group)
     if stream is None:
         stream = torch.cuda.current_stream(d_queries.device)
     elif not isinstance(stream, torch.cuda.Stream):
         stream = torch.cuda.ExternalStream(int(stream), device=d_queries.device)
     with torch.cuda.stream(stream):
-        world = dist.get_world_size(group) if exchange is None else None
         Q = d_queries.shape[0]
-        if exchange is not None:
-            world = int(exchange.world)  # type: ignore[attr-defined]
-        total = n_docs_total if n_docs_total is not None else (
-            _global_docs(index, d_queries.device, group) if exchange is None else None)
-        if total is not None and k > total:
-            raise ValueError(f"kth(={total - k}) out of bounds ({total})")
-        S = index.sample_width(k, world, shard_docs_max)
-        # S > 0: the sample pass zeroes the keys itself (zero_search_kernel)
+        # S > 0: the sample pass writes every key of its own width
         keys = (torch.empty if S > 0 else torch.zeros)((Q, max(S, 1)), dtype=torch.int64,
                                                        device=d_queries.device)
         if S > 0:

@@ -199,7 +199,7 @@ class GpuIndex:
         return v.value
 
     KERNELS = {1: "flat_sample", 2: "flat_rest", 4: "flat_all", 8: "wave_sample",
-               16: "wave_rest", 32: "wave_all"}
+               16: "wave_rest", 32: "wave_all", 64: "large_k"}
 
     def last_dispatch(self) -> dict:
         """What the last search launched (bm25_search_dispatch): the score

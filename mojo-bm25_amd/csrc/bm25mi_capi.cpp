@@ -275,6 +275,25 @@ hipError_t order_ws(bm25_index* h, hipStream_t st) {
 int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, int k,
                int32_t* d_docs, float* d_scores, hipStream_t st) {
   if (Q == 0 || k == 0) return BM25_OK;
+  if (k > kMaxK) {  // any k up to n_docs: the large-k path (bm25mi_large.hip)
+    HIP_TRY(order_ws(h, st), "workspace order");
+    h->ix.disp = Dispatch{};
+    h->ix.disp.sample_p = 1;
+    EventPair* ev = next_events(h);
+    if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
+    HIP_TRY(launch_search_large(h->ix, d_queries, Q, T, k, d_docs, d_scores, st),
+            "large-k search launch");
+    if (ev) {
+      HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
+      HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
+    }
+    HIP_TRY(hipEventRecord(h->ws_done, st), "hipEventRecord");
+    if (h->prof) {
+      h->score_launches += 1;
+      h->searches += 1;
+    }
+    return BM25_OK;
+  }
   int rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
@@ -314,7 +333,6 @@ int check_k(const bm25_index* h, int64_t k, bool shard = false) {
   if (!shard && k > h->ix.n_docs)
     return fail(BM25_EINVAL, "kth(=%lld) out of bounds (%lld)", (long long)(h->ix.n_docs - k),
                 (long long)h->ix.n_docs);
-  if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%lld exceeds the engine limit %d", (long long)k, kMaxK);
   return BM25_OK;
 }
 
@@ -584,7 +602,8 @@ int bm25_sample_width(const bm25_index* h, int64_t shard_docs_max, int32_t world
                       int64_t* width) {
   if (!h || !width) return fail(BM25_EINVAL, "NULL argument");
   if (world < 1 || k < 0) return fail(BM25_EINVAL, "bad world=%d or k=%d", world, k);
-  *width = k == 0 ? 0 : shard_geom(h, shard_docs_max, world, k).S;
+  // k > kMaxK: no sample (each shard's exact top-k, bm25mi_large.hip)
+  *width = (k == 0 || k > kMaxK) ? 0 : shard_geom(h, shard_docs_max, world, k).S;
   return BM25_OK;
 }
 
@@ -595,7 +614,7 @@ int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   if (Q < 0 || T < 0 || world < 1) return fail(BM25_EINVAL, "bad shape");
   int rc = check_k(h, k, true);
   if (rc) return rc;
-  if (Q == 0 || k == 0) return BM25_OK;
+  if (Q == 0 || k == 0 || k > kMaxK) return BM25_OK;  // k > kMaxK: no sample half
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
   rc = ensure_ws(h, Q, T, k);
@@ -623,9 +642,13 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   if (Q == 0 || k == 0) return BM25_OK;
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  const hipStream_t st = (hipStream_t)stream;
+  if (k > kMaxK) {  // this shard's exact top-k (padded past its documents)
+    h->sampled = false;
+    return run_search(h, d_queries, Q, T, k, d_docs, d_scores, st);
+  }
   rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
-  const hipStream_t st = (hipStream_t)stream;
   HIP_TRY(order_ws(h, st), "workspace order");
   const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
   if (!h->sampled) {  // no sample half ran for this search (S = 0)
@@ -762,7 +785,6 @@ int bm25_merge_topk_device(int device, const int32_t* d_docs, const float* d_sco
                            int64_t Q, int32_t k, int32_t* d_out_docs, float* d_out_scores,
                            void* stream) {
   if (W < 1 || Q < 0 || k < 0) return fail(BM25_EINVAL, "bad merge shape W=%lld Q=%lld k=%d", (long long)W, (long long)Q, k);
-  if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%d exceeds the engine limit %d", k, kMaxK);
   HIP_TRY(hipSetDevice(device), "hipSetDevice");
   HIP_TRY(launch_merge_lists(d_docs, d_scores, W, Q, k, Q * (int64_t)k, false, d_out_docs, d_out_scores, (hipStream_t)stream), "merge_lists launch");
   return BM25_OK;
@@ -774,7 +796,6 @@ int bm25_merge_sorted_device(int device, const int32_t* d_docs, const float* d_s
   if (W < 1 || Q < 0 || k < 0 || rank_stride < Q * (int64_t)k)
     return fail(BM25_EINVAL, "bad merge shape W=%lld Q=%lld k=%d stride=%lld", (long long)W,
                 (long long)Q, k, (long long)rank_stride);
-  if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%d exceeds the engine limit %d", k, kMaxK);
   HIP_TRY(hipSetDevice(device), "hipSetDevice");
   HIP_TRY(launch_merge_lists(d_docs, d_scores, W, Q, k, rank_stride, true, d_out_docs,
                              d_out_scores, (hipStream_t)stream),
@@ -1006,7 +1027,6 @@ int bm25_sharded_search(bm25_sharded* s, const int32_t* queries, int64_t Q, int6
   if (k > s->n_docs)
     return fail(BM25_EINVAL, "kth(=%lld) out of bounds (%lld)", (long long)(s->n_docs - k),
                 (long long)s->n_docs);
-  if (k > kMaxK) return fail(BM25_EINVAL, "top_k=%d exceeds the engine limit %d", k, kMaxK);
   if (Q == 0 || k == 0) return BM25_OK;
   if (T > 0 && !queries) return fail(BM25_EINVAL, "NULL queries");
   if (!out_docs || !out_scores) return fail(BM25_EINVAL, "NULL output");

@@ -38,7 +38,8 @@ __host__ __device__ inline uint64_t make_key(float s, uint32_t doc) {
 
 // Exact candidates kept per sample tile.
 constexpr int kTileM = 4;
-// Largest k served.
+// Largest k of the sampled-threshold pipeline; larger k (up to n_docs) take
+// the large-k path (bm25mi_large.hip).
 constexpr int kMaxK = 4096;
 // Merge kernel LDS: number of u64 keys sorted at once.
 constexpr int kMergeP = 8192;
@@ -77,6 +78,7 @@ struct SearchOpts {
 enum {
   kKFlatSample = 1, kKFlatRest = 2, kKFlatAll = 4,
   kKWaveSample = 8, kKWaveRest = 16, kKWaveAll = 32,
+  kKLarge = 64,  // the large-k path (k > kMaxK): dense scores + radix selection
 };
 struct Dispatch {
   uint32_t kernels = 0;       // kK* bits of the score kernels launched
@@ -188,6 +190,27 @@ hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query,
 hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores,
                               int64_t W, int64_t Q, int k, int64_t rank_stride, bool sorted,
                               int32_t* d_out_docs, float* d_out_scores, hipStream_t stream);
+
+// Dense scores of G queries (rows of T terms) into d_out[g * stride + doc];
+// stride >= ntiles << tile_shift (whole tiles are stored; docs past n_docs
+// hold 0).  G <= 65535.
+hipError_t launch_scores_batch(const DevIndex& ix, const int32_t* d_queries, int64_t G, int64_t T,
+                               int64_t stride, float* d_out, hipStream_t stream);
+
+// Exact top-k for any k (the path of k > kMaxK, bm25mi_large.hip): per chunk
+// of queries the dense scores, a radix selection of the k-th key, the keys
+// >= it compacted and sorted.  k > n_docs (a doc shard smaller than k) pads
+// each row with doc -1 / score bits 0xFFFFFFFF.  Device memory is taken
+// stream-ordered (hipMallocAsync) and released at the end of the launch
+// sequence.
+hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                               int k, int32_t* d_docs, float* d_scores, hipStream_t stream);
+// W lists [Q, k] (docs and scores at element w * rank_stride) -> the best k
+// of each query by (score desc, doc asc), for any k (a segmented sort of the
+// W k keys of each query).  Padding (doc -1, score bits ~0) sorts last.
+hipError_t launch_merge_large(const int32_t* d_docs, const float* d_scores, int64_t W, int64_t Q,
+                              int k, int64_t rank_stride, int32_t* d_out_docs,
+                              float* d_out_scores, hipStream_t stream);
 
 // Largest token id of [n] device ids (0 if none is positive) into *d_out.
 hipError_t launch_max_token(const int32_t* d_queries, int64_t n, int32_t* d_out,

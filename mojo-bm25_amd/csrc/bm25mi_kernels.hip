@@ -1278,6 +1278,29 @@ __global__ __launch_bounds__(64) void scores_dense_kernel(IndexArgs a,
   }
 }
 
+// Dense per-doc scores of G queries at once (the large-k path,
+// bm25mi_large.hip): one wave per (tile, query), the whole tile stored to
+// out[g * stride + doc] (stride = ntiles << S: docs past n_docs hold 0).
+template <int S>
+__global__ __launch_bounds__(64) void scores_batch_kernel(IndexArgs a,
+                                                          const int32_t* __restrict__ queries,
+                                                          int32_t T, int64_t stride,
+                                                          float* __restrict__ out) {
+  constexpr int D = 1 << S, E = D / 64;
+  __shared__ __attribute__((aligned(16))) float acc[D];
+  const int64_t tile = blockIdx.x, g = blockIdx.y;
+  zero_acc<S>(acc);
+  add_item<S>(a, tile, queries + g * T, T, acc);
+  float fv[E];
+  take_entries<S>(acc, fv);
+  float* row = out + g * stride + (tile << S);
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int j = 0; j < E / 4; ++j)  // docs 256 j + 4 lane + (0..3) of the tile
+    *reinterpret_cast<float4*>(row + entry_doc(4 * j, lane)) =
+        make_float4(fv[4 * j], fv[4 * j + 1], fv[4 * j + 2], fv[4 * j + 3]);
+}
+
 // ---------------------------------------------------------------------------
 // Index build: u16 accumulator slots + per-(term, tile) segment table, one
 // wave per term.  Terms with at least ntiles/4 postings fill their rel row
@@ -2428,10 +2451,23 @@ hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query, int64
   return hipGetLastError();
 }
 
+hipError_t launch_scores_batch(const DevIndex& ix, const int32_t* d_queries, int64_t G, int64_t T,
+                               int64_t stride, float* d_out, hipStream_t stream) {
+  if (ix.ntiles == 0 || G == 0) return hipSuccess;
+  if (ix.tile_shift != kDefaultTileShift || G > 65535 || stride < (ix.ntiles << ix.tile_shift))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scores_batch_kernel<kDefaultTileShift>, dim3((unsigned)ix.ntiles, (unsigned)G),
+                     dim3(64), 0, stream, args_of(ix), d_queries, (int32_t)T, stride, d_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores, int64_t W,
                               int64_t Q, int k, int64_t rank_stride, bool sorted,
                               int32_t* d_out_docs, float* d_out_scores, hipStream_t stream) {
   if (Q == 0 || k == 0) return hipSuccess;
+  if (k > kMaxK)  // the sort-based merge of the large-k path (bm25mi_large.hip)
+    return launch_merge_large(d_docs, d_scores, W, Q, k, rank_stride, d_out_docs, d_out_scores,
+                              stream);
   if (sorted && W * k <= kMergeSortedCap && W <= 64) {
     hipLaunchKernelGGL(merge_sorted_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, stream,
                        d_docs, d_scores, (int32_t)W, Q, (int32_t)k, rank_stride, d_out_docs,

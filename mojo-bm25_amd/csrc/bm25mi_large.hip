@@ -1,0 +1,394 @@
+// bm25mi_large.hip — exact top-k for any k <= n_docs: the path of k > kMaxK.
+//
+// Replaces bm25_native._topk for large k (bm25_native.py:204-214:
+// argpartition(doc_scores, -k) then argsort of the k survivors, any k <= N;
+// output rows sized [Q, k] at :147-148).  The sampled-threshold pipeline of
+// bm25mi_kernels.hip keeps ~P k keys per query in LDS-sized lists, which is
+// what limits it to k <= kMaxK; above that the selection works on the whole
+// dense score vector, one chunk of G queries at a time:
+//
+//   1. scores_batch_kernel      the chunk's dense fp32 sums [G][Np] (the same
+//                               adds in query-term order as the main path)
+//   2. radix selection          the k-th largest key (score desc, doc asc) of
+//                               every query, 8 bits per pass from the top:
+//                               lk_hist_kernel (LDS histogram of the keys that
+//                               share the prefix decided so far) +
+//                               lk_pick_kernel (the digit holding the k-th key);
+//                               a query is decided as soon as every key with
+//                               its prefix is needed (usually 4-5 passes)
+//   3. lk_compact_kernel        the k keys >= the k-th key (unordered)
+//   4. segmented radix sort     hipCUB, descending (per-query device sort for
+//                               very long rows)
+//   5. lk_write_kernel          keys -> doc ids (+ doc_offset) and scores;
+//                               rows of a shard with fewer than k docs are
+//                               padded with doc -1 / score bits ~0
+//
+// Keys: (sortable score bits) << 32 | (0xFFFFFFFF - doc), as everywhere in
+// the engine (bm25mi_internal.h), so equal scores order by doc ascending and
+// zero-score (untouched) documents fill a row the same way.
+#include "bm25mi_internal.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+namespace bm25mi {
+
+namespace {
+
+struct SelState {
+  uint64_t prefix;  // key bits decided so far (the bits below the pass's digit are 0)
+  uint32_t need;    // rank of the k-th key among the keys that share the prefix
+  uint32_t done;    // 1: every key with the prefix is in the top-k; kth = prefix
+};
+
+__device__ __forceinline__ uint64_t doc_key(float s, uint32_t d) {
+  return ((uint64_t)score_key(s) << 32) | (uint64_t)(0xFFFFFFFFu - d);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+  return v;
+}
+
+// Inclusive prefix sum over the 64 lanes.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(64) void lk_init_kernel(SelState* __restrict__ st, int64_t G,
+                                                     uint32_t k, int32_t* __restrict__ cnt) {
+  for (int64_t g = threadIdx.x; g < G; g += 64) {
+    st[g] = SelState{0ull, k, 0u};
+    cnt[g] = 0;
+  }
+}
+
+// One digit pass: hist[g][digit] += the keys of query g whose bits above
+// (shift + 8) equal its prefix.  Exact zero sums (untouched documents, most
+// of a row) share one digit while shift >= 32 (their doc bits lie below it):
+// they are counted in a register, not with same-address LDS atomics.
+__global__ __launch_bounds__(256) void lk_hist_kernel(const float* __restrict__ scores,
+                                                      int64_t stride, int64_t n_docs, int shift,
+                                                      const SelState* __restrict__ st,
+                                                      uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  const int64_t g = blockIdx.y;
+  const SelState s = st[g];
+  if (s.done) return;  // block-uniform; before the only barriers
+  h[threadIdx.x] = 0u;
+  __syncthreads();
+  const int hs = shift + 8;
+  const uint64_t pre = s.prefix;
+  auto match = [&](uint64_t key) { return hs >= 64 || ((key ^ pre) >> hs) == 0ull; };
+  const bool zfast = shift >= 32;
+  const uint64_t zkey = (uint64_t)score_key(0.f) << 32;
+  const bool zmatch = match(zkey);
+  const uint32_t zdig = (uint32_t)(zkey >> shift) & 255u;
+  const float4* row = reinterpret_cast<const float4*>(scores + g * stride);
+  const int64_t n4 = (n_docs + 3) >> 2;
+  uint32_t zeros = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 f = row[i];
+    const float fe[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t d = 4 * i + c;
+      if (d >= n_docs) break;
+      if (zfast && __float_as_uint(fe[c]) == 0u) {
+        zeros += zmatch ? 1u : 0u;
+        continue;
+      }
+      const uint64_t key = doc_key(fe[c], (uint32_t)d);
+      if (match(key)) atomicAdd(&h[(uint32_t)(key >> shift) & 255u], 1u);
+    }
+  }
+  zeros = wave_sum(zeros);
+  if ((threadIdx.x & 63) == 0 && zeros) atomicAdd(&h[zdig], zeros);
+  __syncthreads();
+  if (h[threadIdx.x]) atomicAdd(&hist[g * 256 + threadIdx.x], h[threadIdx.x]);
+}
+
+// The digit of the pass that holds each query's k-th key (one wave per
+// query): bins scanned from the top; the histogram row is cleared for the
+// next pass.
+__global__ __launch_bounds__(64) void lk_pick_kernel(SelState* __restrict__ st,
+                                                     uint32_t* __restrict__ hist, int shift) {
+  const int64_t g = blockIdx.x;
+  const SelState s = st[g];
+  if (s.done) return;  // wave-uniform; no barriers
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t* h = hist + g * 256;
+  uint32_t c[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    c[j] = h[4 * lane + j];
+    h[4 * lane + j] = 0u;
+  }
+  const uint32_t t = c[0] + c[1] + c[2] + c[3];
+  const uint32_t incl = wave_scan(t);
+  const uint32_t tot = __shfl((int)incl, 63, 64);
+  uint32_t above = tot - incl;  // keys in the bins of the higher lanes
+#pragma unroll
+  for (int j = 3; j >= 0; --j) {
+    if (above < s.need && s.need <= above + c[j]) {  // exactly one (lane, bin)
+      const uint32_t need = s.need - above;
+      SelState n;
+      n.prefix = s.prefix | ((uint64_t)(4 * lane + j) << shift);
+      n.need = need;
+      n.done = (c[j] == need || shift == 0) ? 1u : 0u;
+      st[g] = n;
+    }
+    above += c[j];
+  }
+}
+
+// The keys >= the k-th key of each query (exactly k: keys are unique),
+// appended in any order (one atomic per wave and round).
+__global__ __launch_bounds__(256) void lk_compact_kernel(const float* __restrict__ scores,
+                                                         int64_t stride, int64_t n_docs,
+                                                         const SelState* __restrict__ st,
+                                                         int32_t* __restrict__ cnt,
+                                                         uint64_t* __restrict__ keys, int64_t kk) {
+  const int64_t g = blockIdx.y;
+  const uint64_t kth = st[g].prefix;
+  const uint32_t lane = threadIdx.x & 63;
+  const float4* row = reinterpret_cast<const float4*>(scores + g * stride);
+  const int64_t n4 = (n_docs + 3) >> 2;
+  // every lane of a wave runs the same rounds (ballots below)
+  const int64_t step = (int64_t)gridDim.x * 256;
+  const int64_t rounds = (n4 + step - 1) / step;
+  for (int64_t r = 0; r < rounds; ++r) {
+    const int64_t i = r * step + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    float fe[4] = {0.f, 0.f, 0.f, 0.f};
+    if (i < n4) {
+      const float4 f = row[i];
+      fe[0] = f.x;
+      fe[1] = f.y;
+      fe[2] = f.z;
+      fe[3] = f.w;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t d = 4 * i + c;
+      const uint64_t key = d < n_docs ? doc_key(fe[c], (uint32_t)d) : 0ull;
+      const bool keep = key != 0ull && key >= kth;
+      const uint64_t m = __ballot(keep);
+      if (m == 0ull) continue;
+      int base = 0;
+      if (lane == 0) base = atomicAdd(cnt + g, (int)__popcll(m));
+      base = __shfl(base, 0, 64);
+      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (keep && pos < kk) keys[g * kk + pos] = key;
+    }
+  }
+}
+
+// Keys of W best-first lists -> keys[q][w * k + j] (padding maps to key 0).
+__global__ __launch_bounds__(256) void lk_list_keys_kernel(const int32_t* __restrict__ docs,
+                                                           const float* __restrict__ scores,
+                                                           int64_t W, int64_t q0, int64_t G, int k,
+                                                           int64_t rstride,
+                                                           uint64_t* __restrict__ keys) {
+  const int64_t n = W * k;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < G * n;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t g = e / n, i = e - g * n;
+    const int64_t w = i / k, j = i - w * k;
+    const int64_t o = w * rstride + (q0 + g) * k + j;
+    keys[e] = make_key(scores[o], (uint32_t)docs[o]);
+  }
+}
+
+__global__ __launch_bounds__(64) void lk_offsets_kernel(int* __restrict__ off, int64_t G,
+                                                        int64_t n) {
+  for (int64_t g = threadIdx.x; g <= G; g += 64) off[g] = (int)(g * n);
+}
+
+// Sorted rows [G][n] -> the first k of each: docs (+ doc_offset) and scores
+// of rows q0 .. q0 + G; positions >= k_valid, and key 0, are padding.
+__global__ __launch_bounds__(256) void lk_write_kernel(const uint64_t* __restrict__ keys,
+                                                       int64_t n, int64_t G, int k, int k_valid,
+                                                       int64_t doc_offset,
+                                                       int32_t* __restrict__ docs,
+                                                       float* __restrict__ scores) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < G * k;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t g = e / k, i = e - g * k;
+    const uint64_t key = i < k_valid ? keys[g * n + i] : 0ull;
+    if (key == 0ull) {
+      docs[e] = -1;
+      scores[e] = __uint_as_float(0xFFFFFFFFu);
+    } else {
+      docs[e] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)key) + doc_offset);
+      scores[e] = key_score((uint32_t)(key >> 32));
+    }
+  }
+}
+
+// Rows longer than this are sorted one by one with the device-wide radix
+// sort (the segmented sort gives a row one workgroup).
+constexpr int64_t kSegSortMax = 1 << 20;
+
+// Temporary bytes of sorting G rows of n keys (descending).
+hipError_t sort_bytes(int64_t G, int64_t n, size_t* bytes) {
+  *bytes = 0;
+  if (n > kSegSortMax)
+    return hipcub::DeviceRadixSort::SortKeysDescending(nullptr, *bytes, (const uint64_t*)nullptr,
+                                                       (uint64_t*)nullptr, (int)n, 0, 64, 0);
+  return hipcub::DeviceSegmentedRadixSort::SortKeysDescending(
+      nullptr, *bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(G * n), (int)G,
+      (const int*)nullptr, (const int*)nullptr, 0, 64, 0);
+}
+
+hipError_t sort_rows(const uint64_t* in, uint64_t* out, int64_t G, int64_t n, const int* off,
+                     void* tmp, size_t bytes, hipStream_t st) {
+  if (n > kSegSortMax) {
+    for (int64_t g = 0; g < G; ++g) {
+      const hipError_t e = hipcub::DeviceRadixSort::SortKeysDescending(
+          tmp, bytes, in + g * n, out + g * n, (int)n, 0, 64, st);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  return hipcub::DeviceSegmentedRadixSort::SortKeysDescending(tmp, bytes, in, out, (int)(G * n),
+                                                              (int)G, off, off + 1, 0, 64, st);
+}
+
+// Device memory this path may take per launch sequence.
+int64_t large_budget() {
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 1ull << 30;
+  return std::max<int64_t>(64ll << 20, std::min<int64_t>((int64_t)free_b / 4, 4ll << 30));
+}
+
+// Stream-ordered scratch: released on `st` after everything enqueued so far.
+struct Scratch {
+  hipStream_t st;
+  std::vector<void*> ptrs;
+  explicit Scratch(hipStream_t s) : st(s) {}
+  template <class T>
+  hipError_t get(T** p, int64_t n) {
+    *p = nullptr;
+    const hipError_t e = hipMallocAsync((void**)p, sizeof(T) * (size_t)std::max<int64_t>(n, 1), st);
+    if (e == hipSuccess) ptrs.push_back((void*)*p);
+    return e;
+  }
+  ~Scratch() {
+    for (void* p : ptrs) hipFreeAsync(p, st);
+  }
+};
+
+#define LK_TRY(expr)                    \
+  do {                                  \
+    const hipError_t e_ = (expr);       \
+    if (e_ != hipSuccess) return e_;    \
+  } while (0)
+
+inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cap, (work + per_block - 1) / per_block));
+}
+
+}  // namespace
+
+hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                               int k, int32_t* d_docs, float* d_scores, hipStream_t st) {
+  if (Q == 0 || k == 0) return hipSuccess;
+  ix.disp.kernels |= kKLarge;
+  const int kv = (int)std::min<int64_t>(k, ix.n_docs);  // a doc shard may hold fewer than k
+  if (kv == 0) {  // an empty shard: all padding
+    LK_TRY(hipMemsetAsync(d_docs, 0xFF, sizeof(int32_t) * Q * k, st));
+    return hipMemsetAsync(d_scores, 0xFF, sizeof(float) * Q * k, st);
+  }
+  const int64_t Np = ix.ntiles << ix.tile_shift;  // row stride: whole tiles
+  size_t sb1 = 0;
+  LK_TRY(sort_bytes(1, kv, &sb1));
+  const int64_t per_q = Np * 4 + (int64_t)kv * 16 + 256 * 4 + 64 + (int64_t)sb1 / 4;
+  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));
+  G = std::min<int64_t>(G, 65535);
+  G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / kv - 1));
+  size_t sb = 0;
+  LK_TRY(sort_bytes(G, kv, &sb));
+  Scratch sc(st);
+  float* scores = nullptr;
+  uint32_t* hist = nullptr;
+  SelState* state = nullptr;
+  int32_t* cnt = nullptr;
+  uint64_t *keys = nullptr, *sorted = nullptr;
+  int* off = nullptr;
+  void* tmp = nullptr;
+  LK_TRY(sc.get(&scores, G * Np));
+  LK_TRY(sc.get(&hist, G * 256));
+  LK_TRY(sc.get(&state, G));
+  LK_TRY(sc.get(&cnt, G));
+  LK_TRY(sc.get(&keys, G * kv));
+  LK_TRY(sc.get(&sorted, G * kv));
+  LK_TRY(sc.get(&off, G + 1));
+  LK_TRY(sc.get((char**)&tmp, (int64_t)sb));
+  LK_TRY(hipMemsetAsync(hist, 0, sizeof(uint32_t) * G * 256, st));
+  const int64_t n4 = (ix.n_docs + 3) >> 2;
+  for (int64_t q0 = 0; q0 < Q; q0 += G) {
+    const int64_t g = std::min<int64_t>(G, Q - q0);
+    LK_TRY(launch_scores_batch(ix, d_queries + q0 * T, g, T, Np, scores, st));
+    hipLaunchKernelGGL(lk_init_kernel, dim3(1), dim3(64), 0, st, state, g, (uint32_t)kv, cnt);
+    const dim3 grid(grid_for(n4, 256 * 8, 1024), (unsigned)g);
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      hipLaunchKernelGGL(lk_hist_kernel, grid, dim3(256), 0, st, scores, Np, ix.n_docs, shift,
+                         state, hist);
+      hipLaunchKernelGGL(lk_pick_kernel, dim3((unsigned)g), dim3(64), 0, st, state, hist, shift);
+    }
+    hipLaunchKernelGGL(lk_compact_kernel, grid, dim3(256), 0, st, scores, Np, ix.n_docs, state, cnt,
+                       keys, (int64_t)kv);
+    hipLaunchKernelGGL(lk_offsets_kernel, dim3(1), dim3(64), 0, st, off, g, (int64_t)kv);
+    LK_TRY(sort_rows(keys, sorted, g, kv, off, tmp, sb, st));
+    hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(g * k, 256, 4096)), dim3(256), 0, st, sorted,
+                       (int64_t)kv, g, k, kv, ix.doc_offset, d_docs + q0 * k, d_scores + q0 * k);
+    LK_TRY(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_merge_large(const int32_t* d_docs, const float* d_scores, int64_t W, int64_t Q,
+                              int k, int64_t rank_stride, int32_t* d_out_docs,
+                              float* d_out_scores, hipStream_t st) {
+  if (Q == 0 || k == 0) return hipSuccess;
+  const int64_t n = W * (int64_t)k;
+  if (n > INT32_MAX / 2) return hipErrorInvalidValue;
+  size_t sb1 = 0;
+  LK_TRY(sort_bytes(1, n, &sb1));
+  const int64_t per_q = n * 16 + 64 + (int64_t)sb1 / 4;
+  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));
+  G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / n - 1));
+  size_t sb = 0;
+  LK_TRY(sort_bytes(G, n, &sb));
+  Scratch sc(st);
+  uint64_t *keys = nullptr, *sorted = nullptr;
+  int* off = nullptr;
+  void* tmp = nullptr;
+  LK_TRY(sc.get(&keys, G * n));
+  LK_TRY(sc.get(&sorted, G * n));
+  LK_TRY(sc.get(&off, G + 1));
+  LK_TRY(sc.get((char**)&tmp, (int64_t)sb));
+  for (int64_t q0 = 0; q0 < Q; q0 += G) {
+    const int64_t g = std::min<int64_t>(G, Q - q0);
+    hipLaunchKernelGGL(lk_list_keys_kernel, dim3(grid_for(g * n, 256, 8192)), dim3(256), 0, st,
+                       d_docs, d_scores, W, q0, g, k, rank_stride, keys);
+    hipLaunchKernelGGL(lk_offsets_kernel, dim3(1), dim3(64), 0, st, off, g, n);
+    LK_TRY(sort_rows(keys, sorted, g, n, off, tmp, sb, st));
+    hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(g * k, 256, 4096)), dim3(256), 0, st, sorted,
+                       n, g, k, k, 0ll, d_out_docs + q0 * k, d_out_scores + q0 * k);
+    LK_TRY(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+}  // namespace bm25mi

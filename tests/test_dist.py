@@ -208,3 +208,61 @@ def test_gloo_gather_keys_rank_major(tmp_path):
         want = np.arange(12).reshape(3, 4) + 1000 * r
         want[0, 0] = -1 - r
         assert np.array_equal(g[r], want)
+
+
+class _FakeShard:
+    """The host-side surface of a GpuIndex that sharded_search consults
+    before it launches anything: the shard's documents and its sample width."""
+
+    def __init__(self, n_docs, width):
+        self.n_docs = n_docs
+        self.width = width
+
+    def sample_width(self, k, world, shard_docs_max):
+        return self.width
+
+
+def _checks_worker(rank, world, port, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    try:
+        from bm25mi.dist import _global_docs, sharded_search
+        q = torch.zeros((2, 3), dtype=torch.int32)
+        d = torch.zeros((2, 1), dtype=torch.int32)
+        s = torch.zeros((2, 1), dtype=torch.float32)
+        # k beyond the summed shard documents: numpy's argpartition error
+        ix = _FakeShard(1000 + rank, 8)
+        try:
+            sharded_search(ix, q, 2002, 1001, d, s)
+        except ValueError as e:
+            out["k_err"] = str(e)
+        # the count is cached per process group: a sub-group of rank 0 alone
+        sub = dist.new_group([0])
+        if rank == 0:
+            out["sub_docs"] = _global_docs(ix, q.device, sub)
+        out["world_docs"] = _global_docs(ix, q.device)
+        # ranks whose handles sample different widths: every rank raises
+        try:
+            sharded_search(_FakeShard(1000, 8 + rank), q, 10, 1001, d, s)
+        except ValueError as e:
+            out["width_err"] = str(e)
+        if rank == 0:
+            np.save(result_path, np.array([out], dtype=object), allow_pickle=True)
+        else:
+            assert "width_err" in out and "k_err" in out, out
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_sharded_search_checks(tmp_path):
+    """sharded_search's whole-collection k check and its lazily
+    all-reduced document count (cached per process group), and the sample
+    width agreement across ranks (one all-reduce per group and k)."""
+    out = str(tmp_path / "c.npy")
+    mp.spawn(_checks_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out, allow_pickle=True)[0]  # written by this test's own worker
+    assert got["k_err"] == "kth(=-1) out of bounds (2001)"
+    assert got["sub_docs"] == 1000 and got["world_docs"] == 2001
+    assert "disagree on the sample width" in got["width_err"]

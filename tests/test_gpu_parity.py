@@ -530,10 +530,10 @@ def test_bm25_dense_model_golden(gpu):
 
 
 def test_bm25_top_n_past_kmaxk(gpu):
-    """get_top_n with n > kMaxK (4096) ranks every document like the
-    reference's argsort (bm25.py:172-178): same (score, doc) pairs as the
-    engine's own top-k where they overlap, scores non-increasing, ties by
-    index ascending."""
+    """get_top_n with n > kMaxK (4096) takes the engine's large-k path and
+    ranks like the reference's argsort (bm25.py:172-178): same (score, doc)
+    pairs as the sampled top-k where they overlap, scores non-increasing,
+    ties by index ascending — the order of the dense GPU scores."""
     import bm25
     rng = np.random.default_rng(7)
     words = [f"w{i}" for i in range(60)]
@@ -543,6 +543,7 @@ def test_bm25_top_n_past_kmaxk(gpu):
     q = ["w1", "w7", "w30", "w59"]
     full = m.get_top_n(q, corpus, n=4500)
     assert len(full) == 4500
+    assert "large_k" in m._gpu.last_dispatch()["kernels"]
     sc = np.array([t[0] for t in full])
     assert np.all(np.diff(sc) <= 0)
     top = m.get_top_n(q, corpus, n=100)
