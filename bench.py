@@ -11,7 +11,11 @@ per rank); every rank samples its shard, the sample keys are
 all-gathered over RCCL (one global threshold), every rank lists its keys above
 it, and the per-shard [Q, k] lists are all-gathered and merged on the GPU, so
 every step returns the same global top-k as one GPU would.  Total work is fixed as N
-grows ("scaling": "strong").
+grows ("scaling": "strong").  ``--mode replica`` is the comparison point of
+SURVEY.md §8(e): every rank holds the whole index and searches its Q/N slice of
+the batch with no collective (``--replica-of R`` at N=1 runs rank 0's slice of an
+R-way replica job on one GPU).  ``--config c2`` (a 25.6 MB index, resident in the
+256 MB Infinity Cache) labels its roofline as effective bandwidth.
 
 Printed by rank 0: ONE JSON line with the metric (value = steps x Q / the
 barrier-bracketed wall time, max over ranks), the per-step median from HIP
@@ -98,15 +102,16 @@ def cpu_baseline(args, n_docs, indptr, indices, data, queries, k):
     """BASELINE.md CPU legs on a seeded query sample: (i) one process, one
     core; (ii) a fork-based process pool over the cores this job may use
     (BASELINE.md:54 names the affinity mask; the GPU box gives one GPU's job
-    a share of 16 CPUs — the pool is sized to that share, and the per-core
-    rate scaled to the whole affinity mask is reported beside it, labelled as
-    an extrapolation).  The port is oracle.search_faithful — the reference's
+    a cgroup quota of 16 CPUs — the pool is sized to the quota, or to the
+    affinity mask when no quota is set; BM25_CPU_SHARE caps it explicitly —
+    and the per-core rate scaled to the whole affinity mask is reported
+    beside it, labelled as an extrapolation).  The port is oracle.search_faithful — the reference's
     scipy/numpy call sequence (bm25_native.py:147-158, 204-214)."""
     from oracle import oracle  # the checker / CPU baseline (test infrastructure)
     Q = queries.shape[0]
     quota, aff, why = cpu_quota()
-    share = int(os.environ.get("BM25_CPU_SHARE", "16"))
-    procs = args.cpu_procs if args.cpu_procs > 0 else min(quota, share)
+    share = int(os.environ.get("BM25_CPU_SHARE", "0"))  # explicit cap only
+    procs = args.cpu_procs if args.cpu_procs > 0 else (min(quota, share) if share > 0 else quota)
     nq1 = min(args.cpu_queries, Q)                 # single-core leg
     nqp = min(Q, max(nq1, 4 * procs))              # pool leg: 4 queries per process
     rng = np.random.default_rng(20240601)
@@ -153,11 +158,13 @@ def main():
     ap.add_argument("--cpu-queries", type=int, default=64,
                     help="CPU baseline: seeded query sample size (0 = skip)")
     ap.add_argument("--cpu-procs", type=int, default=-1,
-                    help="CPU baseline pool leg: worker processes (default: the job's CPU "
-                         "share, 16 on the GPU box, or the cgroup quota when smaller)")
+                    help="CPU baseline pool leg: worker processes (default: the cgroup CPU "
+                         "quota, 16 on the GPU box, else the affinity mask)")
     ap.add_argument("--terms", type=int, default=0,
                     help="terms per query (default: the config's, 8); e.g. 16 for the "
                          "long-query workload line")
+    ap.add_argument("--k", type=int, default=0,
+                    help="top-k (default: the config's); k > 4096 takes the large-k path")
     ap.add_argument("--e2e-batches", type=int, default=20,
                     help="host-buffer searches (H2D queries -> D2H results) timed for the "
                          "end-to-end median")
@@ -166,7 +173,17 @@ def main():
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only for "
                          "rehearsing several ranks on one GPU)")
+    ap.add_argument("--mode", default="shard", choices=("shard", "replica"),
+                    help="N > 1: shard = the doc axis split over the ranks (global threshold, "
+                         "two all-gathers); replica = every rank holds the whole index and "
+                         "searches its Q/N slice of the batch, no collective (SURVEY.md §8(e) "
+                         "comparison point)")
+    ap.add_argument("--replica-of", type=int, default=0,
+                    help="replica mode at N=1: run rank 0's slice of an R-way replica job "
+                         "(Q/R queries on the whole index) — the one-GPU proxy of the N=R line")
     args = ap.parse_args()
+    if args.replica_of > 1:
+        args.mode = "replica"
 
     import torch
     from bm25mi import synth
@@ -179,14 +196,21 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     cfg = synth.CONFIGS[args.config]
+    import dataclasses
     if args.terms > 0:
-        import dataclasses
         cfg = dataclasses.replace(cfg, terms_per_query=args.terms)
+    if args.k > 0:
+        cfg = dataclasses.replace(cfg, k=args.k)
     # config 5 holds 6.4B postings: one GPU runs one of the 8 ranks' shards
     # (800M postings, int64 global indptr cut per rank by the generator)
     emul = 8 if (args.config == "c5" and world == 1) else 0
+    replica = args.mode == "replica"
+    if replica and args.config == "c5":
+        raise SystemExit("replica mode holds the whole index per GPU: config 5 does not fit")
     if emul:
         lo, hi = synth.shard_bounds(cfg.n_docs, emul, args.c5_rank)
+    elif replica:
+        lo, hi = 0, cfg.n_docs
     else:
         lo, hi = synth.shard_bounds(cfg.n_docs, world, rank)
     t0 = time.time()
@@ -194,6 +218,13 @@ def main():
     log(f"[rank {rank}] shard docs [{lo},{hi}) nnz={int(indptr[-1])} generated in "
         f"{time.time() - t0:.1f}s")
     queries = synth.make_queries(cfg)
+    q_all = queries.shape[0]
+    if replica:  # this rank's contiguous slice of the batch
+        R = args.replica_of if (args.replica_of > 1 and world == 1) else world
+        r = 0 if args.replica_of > 1 else rank
+        queries = np.ascontiguousarray(queries[q_all * r // R:q_all * (r + 1) // R])
+    else:
+        R = 1
 
     # CPU baseline first (rank 0 at N=1): its process pool forks before this
     # process touches the GPU
@@ -225,7 +256,7 @@ def main():
     sdm = max(b - a for a, b in (synth.shard_bounds(cfg.n_docs, world, r) for r in range(world)))
 
     def step():
-        if world > 1:  # global theta: RCCL all-gathers of sample keys and [Q, k] lists (bm25mi.dist)
+        if world > 1 and not replica:  # global theta: RCCL all-gathers of sample keys and [Q, k] lists (bm25mi.dist)
             sharded_search(index, dq, k, sdm, d_docs, d_scores, None, stream)
         else:
             index.search_device(dq, k, d_docs, d_scores, stream)
@@ -269,29 +300,43 @@ def main():
                "what": "bm25_search host buffers: H2D queries -> search -> D2H docs+scores, "
                        "host clock around the synchronous call"}
     nnz_total = int(indptr[-1])
+    q_done = Q  # queries one step searches on this rank
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-        z = torch.tensor([nnz_total], dtype=torch.int64, device=dev)
-        dist.all_reduce(z)  # the realised postings of every rank's shard
-        nnz_total = int(z.item())
+        if replica:  # every rank holds the whole index; the batch is split
+            z = torch.tensor([Q], dtype=torch.int64, device=dev)
+            dist.all_reduce(z)
+            q_done = int(z.item())
+        else:
+            z = torch.tensor([nnz_total], dtype=torch.int64, device=dev)
+            dist.all_reduce(z)  # the realised postings of every rank's shard
+            nnz_total = int(z.item())
 
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
-    qps = Q * args.steps / elapsed
+    qps = q_done * args.steps / elapsed
     # roofline of the dominant kernel on this rank (rank 0 reports its own)
     alg_bytes = algorithmic_bytes(indptr, queries, k)
     kern_ms = prof["score_ms"] / max(prof["score_launches"], 1)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     shift = int(np.log2(info["tile_docs"]))
-    traffic = load_traffic(args.traffic, args.config, shift, T) if world == 1 else None
+    traffic = (load_traffic(args.traffic, args.config, shift, T)
+               if world == 1 and not replica else None)
+    # an index that fits the 256 MB Infinity Cache (MALL) is not HBM-bound:
+    # its rate is effective bandwidth over algorithmic bytes (config 2)
+    mall = info["device_bytes"] < 256 * 2**20
+    from bm25mi import _capi
 
     if rank == 0:
         out = {
-            "metric": "queries/sec + achieved HBM GB/s, 10M-doc CSC index, batch=1024, k=100"
-            if args.config == "c3" else (f"queries/sec per rank, {cfg.name}, rank "
-                                         f"{args.c5_rank} of 8 (standalone shard search)"
-                                         if emul else f"queries/sec, {cfg.name}"),
+            "metric": ("queries/sec + achieved HBM GB/s, 10M-doc CSC index, batch=1024, k=100"
+                       if args.config == "c3" and not (replica and world == 1 and R > 1) else
+                       (f"queries/sec per rank, {cfg.name}, rank {args.c5_rank} of 8 "
+                        "(standalone shard search)" if emul else
+                        (f"queries/sec per rank, {cfg.name}, rank 0 of a {R}-way replica job "
+                         f"({Q} of {q_all} queries on the whole index)"
+                         if replica and world == 1 and R > 1 else f"queries/sec, {cfg.name}"))),
             "value": round(qps, 2),
             "unit": "queries/s",
             "n_gpus": world,
@@ -301,19 +346,22 @@ def main():
             "ms_per_step_median": round(float(np.median(step_ms)), 4),
             "higher_is_better": True,
             "scaling": "strong",
+            "native_lib": os.path.relpath(_capi.LIB, REPO),
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded Zipf CSC index + df^0.75 queries, csrc/synth.cpp)",
             "config": {
                 "workload": f"{args.config}: {cfg.name}, {T} terms per query" + (
-                    f"; one rank's doc shard [{lo}, {hi}) of the 8-GPU job" if emul else ""),
+                    f"; one rank's doc shard [{lo}, {hi}) of the 8-GPU job" if emul else "") + (
+                    f"; replica mode: {Q} of the {q_all} queries per GPU" if replica else ""),
                 "segments": "sparse" if info.get("sparse") else "dense",
                 "n_docs": cfg.n_docs, "n_terms": cfg.n_terms, "nnz": nnz_total,
                 "batch": Q, "terms_per_query": T, "k": k,
                 "tile_docs": info["tile_docs"],
-                "parallelism": f"doc-shard x{world}" + (
+                "parallelism": (f"replica x{world} (whole index per GPU, batch split, no "
+                                "collective)" if replica else f"doc-shard x{world}" + (
                     f" + {'RCCL' if args.backend == 'nccl' else args.backend} all-gathers "
-                    "(sample keys, packed [Q, k] lists)" if world > 1 else ""),
+                    "(sample keys, packed [Q, k] lists)" if world > 1 else "")),
                 "score_kernels": sorted(dispatch["kernels"]),
                 "term_lanes": dispatch["term_lanes"],
                 "tiles_per_item": dispatch["band_tiles"],
@@ -332,11 +380,19 @@ def main():
                           "score_flat_kernel REST)",
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
-                "scope": "rank 0's shard" if world > 1 else "the whole index",
+                "scope": ("rank 0's query slice" if replica else
+                          "rank 0's shard" if world > 1 else "the whole index"),
+                "note": (f"index of {info['device_bytes'] / 2**20:.1f} MiB fits the 256 MB "
+                         "Infinity Cache (MALL): effective GB/s over algorithmic bytes, not an "
+                         "HBM-bound rate" if mall else None),
             },
             "cpu_baseline": cpu,
             "e2e": e2e,
         }
+        if cfg.k != synth.CONFIGS[args.config].k:  # a --k side line, not the config's metric
+            out["metric"] = f"queries/sec, {args.config} index ({cfg.n_docs} docs) at k={cfg.k}"
+            out["config"]["workload"] += f"; k={cfg.k} instead of the config's " \
+                                         f"{synth.CONFIGS[args.config].k}"
         print(json.dumps(out), flush=True)
     index.close()
     if world > 1:

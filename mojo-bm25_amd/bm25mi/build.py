@@ -13,9 +13,9 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 REPO = os.path.dirname(os.path.dirname(PKG_DIR))
-# BM25MI_LIB: load a variant build instead (dev timing of compile-time knobs,
-# scripts/build_variant.sh); the product library is always libbm25mi.so.
-LIB = os.environ.get("BM25MI_LIB") or os.path.join(PKG_DIR, "libbm25mi.so")
+# The product library.  (scripts/variant_lib_time.py points this at a variant
+# build inside its own child processes before bm25mi._capi is imported.)
+LIB = os.path.join(PKG_DIR, "libbm25mi.so")
 SYNTH_LIB = os.path.join(PKG_DIR, "libbm25synth.so")
 
 HIP_SOURCES = ["bm25mi_kernels.hip", "bm25mi_large.hip", "bm25mi_build.hip", "bm25mi_capi.cpp"]

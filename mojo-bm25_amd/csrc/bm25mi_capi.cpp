@@ -375,7 +375,7 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     if (ip[t + 1] - ip[t] > n_docs)
       return fail(BM25_EINVAL, "column %lld has more entries than n_docs", (long long)t);
   }
-  const int shift = kDefaultTileShift;
+  const int shift = build_tile_shift();
   const int64_t ntiles = (n_docs + (1LL << shift) - 1) >> shift;
   if (ntiles > 65536) return fail(BM25_EINVAL, "n_docs=%lld needs %lld tiles (> 65536)", (long long)n_docs, (long long)ntiles);
 
@@ -857,6 +857,8 @@ int bm25_index_set_option(bm25_index* h, const char* name, int64_t value) {
 
 int bm25_index_get_option(const bm25_index* h, const char* name, int64_t* value) {
   if (!h) return fail(BM25_EINVAL, "NULL index");
+  bm25_index* m = const_cast<bm25_index*>(h);  // the mutex only: set_option writes under it
+  std::lock_guard<std::mutex> lk(m->mu);
   return get_opt(h->ix.opt, name, value);
 }
 

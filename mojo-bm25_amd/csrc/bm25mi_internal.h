@@ -130,7 +130,10 @@ struct Workspace {
                                  // [2] fallback queries, [3] tiles re-scored this search,
                                  // [4] queries left to the block merge (slow)
   int32_t* slow = nullptr;       // [Q] those queries
-  int32_t* wctr = nullptr;       // [kWctrRegions][kWctrInts] item-claim counters, zeroed per search
+  int32_t* wctr = nullptr;       // [kWctrRegions][kWctrInts] item-claim counters: zeroed once
+                                 // at allocation; the last wave of each counter's sharers
+                                 // re-zeroes it (and its finished count) at the end of every
+                                 // flat launch, so each launch finds its region zeroed
   uint64_t* seg = nullptr;       // sparse index: [Q][tiles/8][TT][8] segment of each (query,
                                  // term position, tile) (start | len << 32), built per search
   int64_t cap_seg = 0;           // u64 entries of seg
@@ -216,8 +219,9 @@ hipError_t launch_merge_large(const int32_t* d_docs, const float* d_scores, int6
 hipError_t launch_max_token(const int32_t* d_queries, int64_t n, int32_t* d_out,
                             hipStream_t stream);
 
-// Tile shifts with compiled kernels.
+// Tile shifts with compiled kernels, and the one a new index takes.
 bool tile_shift_supported(int s);
+int build_tile_shift();
 
 // GPU index build (bm25mi_build.hip): scoring rules of bm25_build_scores.
 enum { kLucene = 0, kBm25Py = 1 };

@@ -276,6 +276,28 @@ __device__ __forceinline__ void add_item(const IndexArgs& a, int64_t tile,
 #define BM25_ZA(o) "ds_write_addtid_b32 %2 offset:" #o "\n"
 template <int S>
 __device__ __forceinline__ void zero_acc(float* acc) {
+  if constexpr (S == 12) {  // (variant builds: 4096-doc tiles) as below, 64 stores
+    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)acc;
+    uint32_t m0_saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 1\n"
+                 BM25_ZA(0) BM25_ZA(256) BM25_ZA(512) BM25_ZA(768) BM25_ZA(1024) BM25_ZA(1280)
+                 BM25_ZA(1536) BM25_ZA(1792) BM25_ZA(2048) BM25_ZA(2304) BM25_ZA(2560) BM25_ZA(2816)
+                 BM25_ZA(3072) BM25_ZA(3328) BM25_ZA(3584) BM25_ZA(3840) BM25_ZA(4096) BM25_ZA(4352)
+                 BM25_ZA(4608) BM25_ZA(4864) BM25_ZA(5120) BM25_ZA(5376) BM25_ZA(5632) BM25_ZA(5888)
+                 BM25_ZA(6144) BM25_ZA(6400) BM25_ZA(6656) BM25_ZA(6912) BM25_ZA(7168) BM25_ZA(7424)
+                 BM25_ZA(7680) BM25_ZA(7936) BM25_ZA(8192) BM25_ZA(8448) BM25_ZA(8704) BM25_ZA(8960)
+                 BM25_ZA(9216) BM25_ZA(9472) BM25_ZA(9728) BM25_ZA(9984) BM25_ZA(10240) BM25_ZA(10496)
+                 BM25_ZA(10752) BM25_ZA(11008) BM25_ZA(11264) BM25_ZA(11520) BM25_ZA(11776)
+                 BM25_ZA(12032) BM25_ZA(12288) BM25_ZA(12544) BM25_ZA(12800) BM25_ZA(13056)
+                 BM25_ZA(13312) BM25_ZA(13568) BM25_ZA(13824) BM25_ZA(14080) BM25_ZA(14336)
+                 BM25_ZA(14592) BM25_ZA(14848) BM25_ZA(15104) BM25_ZA(15360) BM25_ZA(15616)
+                 BM25_ZA(15872) BM25_ZA(16128)
+                 "s_mov_b32 m0, %0\n\ts_nop 1"
+                 : "=&s"(m0_saved)
+                 : "s"(la), "v"(0.f)
+                 : "memory");
+    return;
+  }
   if constexpr (S == 11) {
     // ds_write_addtid_b32 stores lane l at M0 + offset + 4 l: no address VGPR
     // to move, 2 cycles per 256 B (128 B/clk/CU, vs ~79 for ds_write_b128);
@@ -284,6 +306,19 @@ __device__ __forceinline__ void zero_acc(float* acc) {
     // M0 is the compiler's (it sets it for its own lane-select uses): saved
     // and restored here.  An M0 write needs a wait state before an
     // instruction reads M0 (without it the first store used a stale M0).
+    //
+    // Why stores the compiler cannot see are safe here: the LDS executes one
+    // wave's LDS instructions in issue order (reads, writes and atomics
+    // alike; lgkmcnt only tracks when their results come back), and an LDS
+    // write has no result to wait for.  So (1) every LDS read the compiler
+    // issued before this block — the epilogue's reads of the tile — reads its
+    // data before these stores overwrite it, whether or not its lgkmcnt wait
+    // has retired yet, and its returned value is unaffected; (2) every LDS
+    // access issued after the block (the next tile's row reads and writes)
+    // executes after all 32 stores, so it sees the zeros.  The "memory"
+    // clobber keeps the compiler from moving its own LDS accesses across the
+    // block.  Nothing else writes this wave's slice: the accumulator is
+    // wave-private (no other wave, no barrier).
     uint32_t m0_saved;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 1\n"
                  BM25_ZA(0) BM25_ZA(256) BM25_ZA(512) BM25_ZA(768) BM25_ZA(1024) BM25_ZA(1280)
@@ -2031,7 +2066,14 @@ __global__ __launch_bounds__(256) void merge_sorted_kernel(
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-bool tile_shift_supported(int s) { return s == kDefaultTileShift; }
+// Tile shift of this build (BM25_TILE_SHIFT: 11 = 2048-doc tiles, the product;
+// 12 = 4096-doc tiles, a variant build for scripts/variant_lib_time.py).
+#ifndef BM25_TILE_SHIFT
+#define BM25_TILE_SHIFT 11
+#endif
+static_assert(BM25_TILE_SHIFT == 11 || BM25_TILE_SHIFT == 12, "2048- or 4096-doc tiles");
+bool tile_shift_supported(int s) { return s == BM25_TILE_SHIFT; }
+int build_tile_shift() { return BM25_TILE_SHIFT; }
 
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int32_t* d_err,
                                hipStream_t stream) {
@@ -2139,13 +2181,16 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
   auto go = [&](auto kern) {
     int grid = persistent_grid(kern, 64);
     if (sg.nq_dev) grid = std::min(grid, 8 * kFallbackBlocks);  // fallback: usually no queries
+    // every claim counter of an XCD range needs a wave: counter cm is served
+    // by the workgroups with (blockIdx / 8) % claim_m == cm
+    const int claim_m = std::max(1, std::min(ix.opt.claim_m, grid / 8));
     const int bw = flat_band(ix.opt, nt, sg.nq_host, grid, 64 >> TL, sg.nq_dev != nullptr);
     ix.disp.kernels |= PH == kSample ? kKFlatSample : (PH == kRest ? kKFlatRest : kKFlatAll);
     ix.disp.term_lanes = 1 << TL;
     ix.disp.band_tiles[PH] = bw;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, st, a, q, (int32_t)T, sg.P,
                        sg.G, sg.nq_host, sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, sg.cstride,
-                       ws.list, ws.list_cnt, ws.list_cap, wctr, ix.opt.claim_ch, ix.opt.claim_m,
+                       ws.list, ws.list_cnt, ws.list_cap, wctr, ix.opt.claim_ch, claim_m,
                        skip ? sg.sample_keys : nullptr, sg.sample_stride, bw,
                        PH == kSample && SM == 1 ? sg.cand_mirror : nullptr);
   };
@@ -2339,7 +2384,7 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
 
 #define BM25_SHIFT_DISPATCH(call)                        \
   switch (ix.tile_shift) {                               \
-    case kDefaultTileShift: call(kDefaultTileShift); break; \
+    case BM25_TILE_SHIFT: call(BM25_TILE_SHIFT); break;    \
     default: return hipErrorInvalidValue;                \
   }
 
@@ -2445,8 +2490,8 @@ hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries, int64_t Q
 hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query, int64_t T,
                                float* d_out, hipStream_t stream) {
   if (ix.ntiles == 0) return hipSuccess;
-  if (ix.tile_shift != kDefaultTileShift) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(scores_dense_kernel<kDefaultTileShift>, dim3((unsigned)ix.ntiles), dim3(64),
+  if (ix.tile_shift != BM25_TILE_SHIFT) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scores_dense_kernel<BM25_TILE_SHIFT>, dim3((unsigned)ix.ntiles), dim3(64),
                      0, stream, args_of(ix), d_query, (int32_t)T, d_out);
   return hipGetLastError();
 }
@@ -2454,9 +2499,9 @@ hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query, int64
 hipError_t launch_scores_batch(const DevIndex& ix, const int32_t* d_queries, int64_t G, int64_t T,
                                int64_t stride, float* d_out, hipStream_t stream) {
   if (ix.ntiles == 0 || G == 0) return hipSuccess;
-  if (ix.tile_shift != kDefaultTileShift || G > 65535 || stride < (ix.ntiles << ix.tile_shift))
+  if (ix.tile_shift != BM25_TILE_SHIFT || G > 65535 || stride < (ix.ntiles << ix.tile_shift))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(scores_batch_kernel<kDefaultTileShift>, dim3((unsigned)ix.ntiles, (unsigned)G),
+  hipLaunchKernelGGL(scores_batch_kernel<BM25_TILE_SHIFT>, dim3((unsigned)ix.ntiles, (unsigned)G),
                      dim3(64), 0, stream, args_of(ix), d_queries, (int32_t)T, stride, d_out);
   return hipGetLastError();
 }

@@ -9,6 +9,8 @@ CHILD = r'''
 import json, os, sys, numpy as np
 sys.path[:0] = [os.path.join(sys.argv[1], "mojo-bm25_amd"), sys.argv[1]]
 import torch
+import bm25mi.build
+bm25mi.build.LIB = os.environ["VLIB"]  # this child's variant library
 from bm25mi import synth, _capi
 from bm25mi.index import GpuIndex
 cfg = synth.CONFIGS[os.environ.get("VCFG", "c3")]
@@ -36,7 +38,7 @@ print(json.dumps({"lib": os.path.basename(_capi.LIB), "env": os.environ.get("VEN
 '''
 for arg in sys.argv[1:]:  # LIB[:NAME=VAL,NAME=VAL]: per-library environment
     lib, _, kv = arg.partition(":")
-    env = dict(os.environ, BM25MI_LIB=os.path.abspath(lib))
+    env = dict(os.environ, VLIB=os.path.abspath(lib))
     env.update(dict(x.split("=", 1) for x in kv.split(",") if x))
     env["VENV"] = kv
     r = subprocess.run(["timeout", "-k", "10", "240", sys.executable, "-c", CHILD, REPO], env=env,

@@ -805,6 +805,23 @@ def test_build_scores_rejects_bad_triples(gpu):
         build_scores([0, 5], [1, 1], [1.0, 2.0], [3, 3], 2)
     with pytest.raises(ValueError, match="positive"):
         build_scores([0], [1], [0.0], [3], 2)
+    # ids that would index doc_len / idf out of bounds stop the
+    # build before scoring — negative ids and ids near 2^30, docs and terms
+    rng = np.random.default_rng(5)
+    n = 50_000
+    docs = rng.integers(0, 1000, n).astype(np.int32)
+    terms = rng.integers(0, 30, n).astype(np.int32)
+    tfs = np.ones(n, np.float32)
+    dl = np.full(1000, 7, np.int32)
+    for bad_d, bad_t in ((-1, None), (-(1 << 30), None), ((1 << 30) - 1, None), (1 << 30, None),
+                         (None, -1), (None, (1 << 30) + 7), (None, 2**31 - 1)):
+        d2, t2 = docs.copy(), terms.copy()
+        if bad_d is not None:
+            d2[n // 2] = bad_d
+        if bad_t is not None:
+            t2[n - 1] = bad_t
+        with pytest.raises(ValueError, match="out of range"):
+            build_scores(d2, t2, tfs, dl, 30)
     ip, ix, dt = build_scores([], [], [], [0, 0], 4)
     assert np.array_equal(ip, np.zeros(5, np.int64)) and ix.size == 0
 
