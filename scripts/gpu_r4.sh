@@ -26,8 +26,8 @@ for step in ${STEPS:-tests lines}; do
     ;;
   variants)  # VLIBS: variant libraries timed against the product (scripts/variant_lib_time.py)
     for cfg in ${VCFGS:-c3}; do
-      VCFG=$cfg timeout -k 10 900 python -u scripts/variant_lib_time.py mojo-bm25_amd/bm25mi/libbm25mi.so $VLIBS > $OUT/variants_$cfg.jsonl 2> $OUT/variants_$cfg.err || { echo variants failed; tail -20 $OUT/variants_$cfg.err; exit 1; }
-      cat $OUT/variants_$cfg.jsonl
+      VCFG=${cfg%%:*} VTERMS=$([ "${cfg#*:}" != "$cfg" ] && echo ${cfg#*:}) timeout -k 10 900 python -u scripts/variant_lib_time.py $VLIBS > $OUT/variants_${cfg/:/_t}.jsonl 2> $OUT/variants_${cfg/:/_t}.err || { echo variants failed; tail -20 $OUT/variants_${cfg/:/_t}.err; exit 1; }
+      cat $OUT/variants_${cfg/:/_t}.jsonl
     done
     ;;
   esac

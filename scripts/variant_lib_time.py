@@ -9,17 +9,22 @@ CHILD = r'''
 import json, os, sys, numpy as np
 sys.path[:0] = [os.path.join(sys.argv[1], "mojo-bm25_amd"), sys.argv[1]]
 import torch
-import bm25mi.build
-bm25mi.build.LIB = os.environ["VLIB"]  # this child's variant library
+import importlib  # (bm25mi.build as an attribute is the build() function)
+importlib.import_module("bm25mi.build").LIB = os.environ["VLIB"]  # this child's variant library
 from bm25mi import synth, _capi
 from bm25mi.index import GpuIndex
 cfg = synth.CONFIGS[os.environ.get("VCFG", "c3")]
+if os.environ.get("VTERMS"):
+    import dataclasses
+    cfg = dataclasses.replace(cfg, terms_per_query=int(os.environ["VTERMS"]))
 c = "/tmp/vt_" + cfg.name.split()[0]
+# config 5: one rank's doc shard (rank 0 of 8), as bench.py --config c5
+lo, hi = synth.shard_bounds(cfg.n_docs, 8, 0) if os.environ.get("VCFG") == "c5" else (0, cfg.n_docs)
 if not os.path.exists(c + "_dt.npy"):
-    ip, ix, dt = synth.make_index(cfg, threads=16)
+    ip, ix, dt = synth.make_index(cfg, lo, hi, threads=16)
     for n, a in (("ip", ip), ("ix", ix), ("dt", dt)): np.save(c + "_" + n + ".npy", a)
 ip, ix, dt = (np.load(c + "_" + n + ".npy", mmap_mode="r") for n in ("ip", "ix", "dt"))
-index = GpuIndex(np.ascontiguousarray(ip), ix, dt, cfg.n_docs)
+index = GpuIndex(np.ascontiguousarray(ip), ix, dt, hi - lo, doc_offset=lo)
 q = torch.from_numpy(synth.make_queries(cfg)).cuda()
 Q, k = q.shape[0], cfg.k
 d = torch.empty((Q, k), dtype=torch.int32, device="cuda"); s = torch.empty((Q, k), device="cuda")
@@ -33,7 +38,8 @@ for _ in range(20):
 p = index.profile_read()
 torch.cuda.synchronize()
 h = int((d.to(torch.int64) * 1000003 + s.view(torch.int32).to(torch.int64)).sum().item())
-print(json.dumps({"lib": os.path.basename(_capi.LIB), "env": os.environ.get("VENV", ""), "score_ms": round(p["score_ms"] / p["score_launches"], 4),
+print(json.dumps({"lib": os.path.basename(_capi.LIB), "env": os.environ.get("VENV", ""),
+                  "cfg": os.environ.get("VCFG", "c3"), "terms": cfg.terms_per_query, "score_ms": round(p["score_ms"] / p["score_launches"], 4),
                   "total_ms": round(p["total_ms"] / p["searches"], 4), "hash": h}), flush=True)
 '''
 for arg in sys.argv[1:]:  # LIB[:NAME=VAL,NAME=VAL]: per-library environment
