@@ -30,6 +30,10 @@ for step in ${STEPS:-tests lines}; do
       cat $OUT/variants_${cfg/:/_t}.jsonl
     done
     ;;
+  probe)  # per-rank config-3 shard work with real sample keys + modelled collectives
+    timeout -k 10 900 python -u scripts/shard_probe.py ${PROBE_WS:-1 2 4 8} > $OUT/shard_probe.jsonl 2> $OUT/shard_probe.err || { echo probe failed; tail -20 $OUT/shard_probe.err; exit 1; }
+    cat $OUT/shard_probe.jsonl
+    ;;
   esac
 done
 exit 0
