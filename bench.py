@@ -321,8 +321,10 @@ def main():
     kern_ms = prof["score_ms"] / max(prof["score_launches"], 1)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     shift = int(np.log2(info["tile_docs"]))
+    default_k = cfg.k == synth.CONFIGS[args.config].k
     traffic = (load_traffic(args.traffic, args.config, shift, T)
-               if world == 1 and not replica else None)
+               if world == 1 and not replica and default_k else None)
+    large_k = "large_k" in dispatch["kernels"]
     # an index that fits the 256 MB Infinity Cache (MALL) is not HBM-bound:
     # its rate is effective bandwidth over algorithmic bytes (config 2)
     mall = info["device_bytes"] < 256 * 2**20
@@ -376,8 +378,10 @@ def main():
                 "traffic_source": (f"profiles/traffic.json ({traffic.get('source')}): "
                                    f"{traffic.get('method')}; L2 hit rate "
                                    f"{traffic.get('l2_hit_rate')}") if traffic else None,
-                "kernel": "score pass (score_flat_kernel SAMPLE + theta_wave_kernel + "
-                          "score_flat_kernel REST)",
+                "kernel": ("large-k search (scores_batch_kernel dense sums + lk_* radix "
+                           "selection + hipCUB segmented sort)" if large_k else
+                           "score pass (score_flat_kernel SAMPLE + theta_wave_kernel + "
+                           "score_flat_kernel REST)"),
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
                 "scope": ("rank 0's query slice" if replica else

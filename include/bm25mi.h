@@ -199,9 +199,11 @@ int bm25_merge_sorted_device(int device, const int32_t* d_docs,
  *   bm25_sample_width(idx, shard_docs_max, world, k, &S): keys per query each
  *     rank samples (the same on every rank: shard_docs_max = the largest
  *     shard's document count; S = 0: shards too small to sample, or
- *     k > 4096 — then the finish half lists the shard's exact top-k);
+ *     k > 4096 — then the finish half lists the shard's exact top-k; S = k
+ *     with the theta_bound option: tile-bound keys);
  *   bm25_search_sample_device(...): this shard's sample keys -> d_keys
- *     (u64 [Q][S], zero-padded);
+ *     (u64 [Q][S], zero-padded: a SAMPLE pass, or — theta_bound — the best S
+ *     tile-bound keys, read from the tile bounds without scoring);
  *   (caller) all-gather d_keys of every rank -> d_all_keys [world][Q][S];
  *   bm25_search_finish_device(...): theta = the k-th best key of the world's
  *     sample (k real documents score at least this), then every key >= theta
@@ -271,11 +273,18 @@ int bm25_profile_read(bm25_index* idx, double* score_ms_total,
  */
 int bm25_search_stats(bm25_index* idx, int64_t* rescored_tiles,
                       int64_t* fallback_queries);
+/* The same plus *bound_skipped: (query, tile) pairs the REST pass skipped
+ * because the sum of the query terms' largest scores in the tile (the tile
+ * bounds of a dense, non-negative index) is below the query's threshold.
+ * Any pointer may be NULL. */
+int bm25_search_stats_ex(bm25_index* idx, int64_t* rescored_tiles,
+                         int64_t* fallback_queries, int64_t* bound_skipped);
 
 /*
  * Search options of one handle.  A new handle takes them from the
  * environment (BM25_FLAT, BM25_FLAT_BW, BM25_ITEMS_PER_WAVE, BM25_SAMPLE_P,
- * BM25_LIST_CAP, BM25_CLAIM_CH, BM25_CLAIM_M) at bm25_index_create; these
+ * BM25_LIST_CAP, BM25_CLAIM_CH, BM25_CLAIM_M, BM25_TILE_BOUND, BM25_THETA_BOUND) at
+ * bm25_index_create; these
  * calls change or read them afterwards, effective from the next search.
  * Results never depend on them (every setting is bit-exact); they choose
  * kernels and geometry:
@@ -290,6 +299,15 @@ int bm25_search_stats(bm25_index* idx, int64_t* rescored_tiles,
  *                    values force queries through the exact fallback stage)
  *   "claim_ch", "claim_m"  flat-kernel item claims: items per claim (1),
  *                    counters per XCD (4)
+ *   "tile_bound"     1 (default): the REST pass skips tiles whose query-term
+ *                    maxima (f16 bounds kept per (term, tile) by a dense,
+ *                    non-negative index) sum below the threshold;
+ *                    0: every tile is scored
+ *   "theta_bound"    1 (default): the threshold comes from those tile bounds
+ *                    (per tile, its largest query-term maximum is a real
+ *                    document's score lower bound) with no SAMPLE pass;
+ *                    0: the sampled threshold.  Every shard of a multi-rank
+ *                    search needs the same setting (bm25_sample_width)
  * Replaces no reference call (the reference has no tuning surface; its MAX
  * custom op takes compile-time parameters, graph.py:72).
  */
@@ -300,10 +318,12 @@ int bm25_index_get_option(const bm25_index* idx, const char* name, int64_t* valu
  * What the last search on the handle launched (diagnostics, no device wait):
  *   *kernels     bit mask of score kernels: 1 flat SAMPLE, 2 flat REST,
  *                4 flat ALL (exact pass / fallback stage), 8 wave SAMPLE,
- *                16 wave REST, 32 wave ALL
+ *                16 wave REST, 32 wave ALL, 64 large-k path, 128 tile-bound
+ *                threshold keys
  *   *term_lanes  flat kernel: term lanes per tile (8, 16, 32 or 64)
  *   band_tiles   [3]: flat kernel tiles per item of ALL, SAMPLE, REST
- *   *sample_p    sampling stride of the search (1: exact pass)
+ *   *sample_p    sampling stride of the search (1: exact pass, 0: tile-bound
+ *                threshold keys, no SAMPLE pass)
  * Any pointer may be NULL.
  */
 int bm25_search_dispatch(bm25_index* idx, uint32_t* kernels, int32_t* term_lanes,

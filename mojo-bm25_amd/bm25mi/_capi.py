@@ -63,6 +63,7 @@ _SIGS = {
     "bm25_profile_enable": ([_P, ctypes.c_int], ctypes.c_int),
     "bm25_profile_read": ([_P, _PD, _PI64, _PD, _PI64, _PI64], ctypes.c_int),
     "bm25_search_stats": ([_P, _PI64, _PI64], ctypes.c_int),
+    "bm25_search_stats_ex": ([_P, _PI64, _PI64, _PI64], ctypes.c_int),
     "bm25_index_set_option": ([_P, ctypes.c_char_p, _I64], ctypes.c_int),
     "bm25_index_get_option": ([_P, ctypes.c_char_p, _PI64], ctypes.c_int),
     "bm25_search_dispatch": ([_P, ctypes.POINTER(ctypes.c_uint32), _PI32, _PI32, _PI32],

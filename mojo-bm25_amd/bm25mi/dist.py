@@ -97,8 +97,9 @@ def _global_docs(index, device, group=None) -> int:
 
 def _agree_width(index, S: int, k: int, device, group=None) -> None:
     """Every rank must sample the same width S (the key all-gather has one
-    shape): it depends on k, the world and the handle's ``sample_p`` option,
-    which each rank sets on its own.  Checked once per (group, k) by one
+    shape): it depends on k, the world and the handle's ``sample_p`` and
+    ``theta_bound`` options (and on the shard having tile bounds), which each
+    rank sets on its own.  Checked once per (group, k) by one
     all-reduce of (S, -S) with MAX; every rank raises the same ValueError when
     they differ."""
     seen = index.__dict__.setdefault("_bm25_width_ok", set())
@@ -111,7 +112,8 @@ def _agree_width(index, S: int, k: int, device, group=None) -> None:
     lo, hi = -int(t[1].item()), int(t[0].item())
     if lo != hi:
         raise ValueError(f"ranks disagree on the sample width at k={k} (min {lo}, max {hi}): "
-                         "set the same sample_p option on every rank's index")
+                         "set the same sample_p and theta_bound options on every rank's index "
+                         "(theta_bound needs every shard's tile bounds: dense, non-negative)")
     seen.add(key)
 
 

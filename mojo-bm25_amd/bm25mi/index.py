@@ -190,7 +190,8 @@ class GpuIndex:
     # ------------------------------------------------------------------
     def set_option(self, name: str, value: int) -> None:
         """A search option of this handle (bm25_index_set_option: flat,
-        flat_bw, items_per_wave, sample_p, list_cap, claim_ch, claim_m)."""
+        flat_bw, items_per_wave, sample_p, list_cap, claim_ch, claim_m,
+        tile_bound, theta_bound)."""
         check(lib.bm25_index_set_option(self._h, name.encode(), int(value)))
 
     def get_option(self, name: str) -> int:
@@ -199,7 +200,7 @@ class GpuIndex:
         return v.value
 
     KERNELS = {1: "flat_sample", 2: "flat_rest", 4: "flat_all", 8: "wave_sample",
-               16: "wave_rest", 32: "wave_all", 64: "large_k"}
+               16: "wave_rest", 32: "wave_all", 64: "large_k", 128: "bound_keys"}
 
     def last_dispatch(self) -> dict:
         """What the last search launched (bm25_search_dispatch): the score
@@ -218,11 +219,14 @@ class GpuIndex:
 
     def search_stats(self) -> dict:
         """Selection statistics of the last search: tiles re-scored exactly,
-        queries sent to the exact fallback stage."""
+        queries sent to the exact fallback stage, (query, tile) pairs the REST
+        pass skipped by their tile bound."""
         r = ctypes.c_int64()
         f = ctypes.c_int64()
-        check(lib.bm25_search_stats(self._h, ctypes.byref(r), ctypes.byref(f)))
-        return {"rescored_tiles": r.value, "fallback_queries": f.value}
+        b = ctypes.c_int64()
+        check(lib.bm25_search_stats_ex(self._h, ctypes.byref(r), ctypes.byref(f), ctypes.byref(b)))
+        return {"rescored_tiles": r.value, "fallback_queries": f.value,
+                "bound_skipped_tiles": b.value}
 
 
 def merge_topk_device(device: int, d_docs, d_scores, W: int, Q: int, k: int, d_out_docs,

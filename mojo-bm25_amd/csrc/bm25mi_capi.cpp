@@ -117,6 +117,8 @@ SearchOpts env_opts() {
   o.list_cap = env_int("BM25_LIST_CAP", o.list_cap);
   o.claim_ch = env_int("BM25_CLAIM_CH", o.claim_ch);
   o.claim_m = env_int("BM25_CLAIM_M", o.claim_m);
+  o.tile_bound = env_int("BM25_TILE_BOUND", o.tile_bound) != 0;
+  o.theta_bound = env_int("BM25_THETA_BOUND", o.theta_bound) != 0;
   return o;
 }
 
@@ -146,6 +148,12 @@ int set_opt(SearchOpts& o, const char* name, int64_t v) {
   } else if (n == "claim_m") {
     if (v < 1 || v > kClaimM) return fail(BM25_EINVAL, "claim_m must be in 1..%d", kClaimM);
     o.claim_m = (int)v;
+  } else if (n == "tile_bound") {
+    if (v != 0 && v != 1) return fail(BM25_EINVAL, "tile_bound must be 0 or 1");
+    o.tile_bound = (int)v;
+  } else if (n == "theta_bound") {
+    if (v != 0 && v != 1) return fail(BM25_EINVAL, "theta_bound must be 0 or 1");
+    o.theta_bound = (int)v;
   } else {
     return fail(BM25_EINVAL, "unknown option '%s'", name);
   }
@@ -162,6 +170,8 @@ int get_opt(const SearchOpts& o, const char* name, int64_t* v) {
   else if (n == "list_cap") *v = o.list_cap;
   else if (n == "claim_ch") *v = o.claim_ch;
   else if (n == "claim_m") *v = o.claim_m;
+  else if (n == "tile_bound") *v = o.tile_bound;
+  else if (n == "theta_bound") *v = o.theta_bound;
   else return fail(BM25_EINVAL, "unknown option '%s'", name);
   return BM25_OK;
 }
@@ -297,7 +307,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   int rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
-  const int P = sample_geom(h->ix.ntiles, k, 1, h->ix.opt.sample_p).P;
+  const int P = search_geom(h->ix, h->ix.ntiles, k, 1).P;
   h->ix.disp = Dispatch{};
   h->ix.disp.sample_p = P;
   EventPair* ev = next_events(h);
@@ -317,7 +327,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
 
 // Counters of the last search (caller holds h->mu); the search may run on a
 // caller's stream: wait for its end event (ws_done), not for the device.
-void read_counters(bm25_index* h, int32_t (&cnt)[4]) {
+void read_counters(bm25_index* h, int32_t (&cnt)[kCounters]) {
   if (!h->ws.counters) return;
   if (h->ws_done) hipEventSynchronize(h->ws_done);
   hipMemcpyAsync(cnt, h->ws.counters, sizeof cnt, hipMemcpyDeviceToHost, h->stream);
@@ -475,6 +485,17 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
   ix.nonneg = true;
   for (int64_t p = 0; p < nnz && ix.nonneg; ++p)
     ix.nonneg = data[p] == 0.0f || data[p] >= 1.17549435e-38f;
+  // tile bounds of the REST pass (dense table, non-negative index); without
+  // the memory the search simply runs without them
+  if (!ix.sparse && ix.nonneg && n_terms > 0 && ntiles > 0) {
+    if (hipMalloc(&ix.bmax, sizeof(uint16_t) * n_terms * ntiles) == hipSuccess) {
+      TRYC(launch_build_bmax(ix, h->stream), "build_bmax launch");
+      h->device_bytes += (int64_t)(sizeof(uint16_t) * n_terms * ntiles);
+    } else {
+      (void)hipGetLastError();
+      ix.bmax = nullptr;
+    }
+  }
   int32_t herr = 0;
   TRYC(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), "D2H err");
   TRYC(hipStreamSynchronize(h->stream), "build sync");
@@ -509,6 +530,7 @@ int bm25_index_destroy(bm25_index* h) {
   hipFree(h->ix.tl_start);
   hipFree(h->ix.ldoc);
   hipFree(h->ix.val);
+  hipFree(h->ix.bmax);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return BM25_OK;
@@ -595,7 +617,7 @@ int bm25_max_token_device(bm25_index* h, const int32_t* d_queries, int64_t Q, in
 static SampleGeom shard_geom(const bm25_index* h, int64_t shard_docs_max, int32_t world, int k) {
   const int64_t D = 1ll << h->ix.tile_shift;
   const int64_t nt = std::max<int64_t>((std::max<int64_t>(shard_docs_max, h->ix.n_docs) + D - 1) / D, 1);
-  return sample_geom(nt, k, std::max(world, 1), h->ix.opt.sample_p);
+  return search_geom(h->ix, nt, k, std::max(world, 1));
 }
 
 int bm25_sample_width(const bm25_index* h, int64_t shard_docs_max, int32_t world, int32_t k,
@@ -820,7 +842,7 @@ int bm25_profile_read(bm25_index* h, double* score_ms_total, int64_t* score_laun
   std::lock_guard<std::mutex> lk(h->mu);
   hipSetDevice(h->ix.device);
   harvest_events(h);
-  int32_t cnt[4] = {0, 0, 0, 0};
+  int32_t cnt[kCounters] = {};
   read_counters(h, cnt);
   if (score_ms_total) *score_ms_total = h->score_ms;
   if (score_launches) *score_launches = h->score_launches;
@@ -831,13 +853,19 @@ int bm25_profile_read(bm25_index* h, double* score_ms_total, int64_t* score_laun
 }
 
 int bm25_search_stats(bm25_index* h, int64_t* rescored_tiles, int64_t* fallback_queries) {
+  return bm25_search_stats_ex(h, rescored_tiles, fallback_queries, nullptr);
+}
+
+int bm25_search_stats_ex(bm25_index* h, int64_t* rescored_tiles, int64_t* fallback_queries,
+                         int64_t* bound_skipped) {
   if (!h) return fail(BM25_EINVAL, "NULL index");
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
-  int32_t cnt[4] = {0, 0, 0, 0};
+  int32_t cnt[kCounters] = {};
   read_counters(h, cnt);
   if (rescored_tiles) *rescored_tiles = cnt[3];
   if (fallback_queries) *fallback_queries = cnt[2];
+  if (bound_skipped) *bound_skipped = cnt[5];
   return BM25_OK;
 }
 

@@ -72,6 +72,9 @@ struct SearchOpts {
   int list_cap = 0;        // candidate-list capacity per query (0: auto)
   int claim_ch = 1;        // flat items per claim
   int claim_m = 4;         // claim counters per XCD (1..kClaimM)
+  int tile_bound = 1;      // REST skips tiles whose term-maxima sum is below theta (needs bmax)
+  int theta_bound = 1;     // threshold keys from the tile bounds instead of a SAMPLE pass
+                           // (needs bmax; search_geom)
 };
 
 // What the last search launched (bm25_search_dispatch).
@@ -79,12 +82,13 @@ enum {
   kKFlatSample = 1, kKFlatRest = 2, kKFlatAll = 4,
   kKWaveSample = 8, kKWaveRest = 16, kKWaveAll = 32,
   kKLarge = 64,  // the large-k path (k > kMaxK): dense scores + radix selection
+  kKBound = 128, // tile-bound threshold keys (bound_keys_kernel) instead of a SAMPLE pass
 };
 struct Dispatch {
   uint32_t kernels = 0;       // kK* bits of the score kernels launched
   int32_t term_lanes = 0;     // flat kernel: term lanes per tile (8, 16, 32, 64)
   int32_t band_tiles[3] = {0, 0, 0};  // flat kernel: tiles per item of ALL, SAMPLE, REST
-  int32_t sample_p = 0;       // sampling stride (1: exact pass)
+  int32_t sample_p = 0;       // sampling stride (1: exact pass, 0: tile-bound keys)
 };
 
 struct DevIndex {
@@ -108,6 +112,11 @@ struct DevIndex {
   int64_t n_pairs = 0;
   uint16_t* ldoc = nullptr;
   float* val = nullptr;
+  // Tile bounds (dense segment table, non-negative index): each (term,
+  // tile)'s largest score as f16 bits rounded DOWN, [V][ntiles] — a lower
+  // bound of that score (threshold keys) and, one f16 step up, an upper bound
+  // (the REST pass's tile skip)
+  uint16_t* bmax = nullptr;
   SearchOpts opt;
   mutable Dispatch disp;  // written by the launchers (callers hold the handle's mutex)
 };
@@ -128,7 +137,8 @@ struct Workspace {
   int32_t* queue = nullptr;      // [Q*maxflag] items = qi*maxflag + i
   int32_t* counters = nullptr;   // [kCounters]: [0]/[1] rescore queue length / pop cursor,
                                  // [2] fallback queries, [3] tiles re-scored this search,
-                                 // [4] queries left to the block merge (slow)
+                                 // [4] queries left to the block merge (slow),
+                                 // [5] (query, tile) pairs REST skipped by their tile bound
   int32_t* slow = nullptr;       // [Q] those queries
   int32_t* wctr = nullptr;       // [kWctrRegions][kWctrInts] item-claim counters: zeroed once
                                  // at allocation; the last wave of each counter's sharers
@@ -146,19 +156,29 @@ inline int64_t maxflag_for(int k, int64_t ntiles) {
   return m < ntiles ? m : (ntiles > 0 ? ntiles : 1);
 }
 
-// Sampling geometry of a search over W doc shards of ntiles tiles each:
+// Threshold geometry of a search over W doc shards of ntiles tiles each:
 // stride P (1 = no sampling), m keys per sample tile, S keys per query per
 // shard, sample tiles in groups of G consecutive tiles (one group per G*P).
+// P = 0: no SAMPLE pass — each shard's S = k best tile-bound keys
+// (bound_keys_kernel).
 struct SampleGeom {
   int P, m;
   int64_t S;
   int G;  // sample tiles come in groups of G consecutive tiles (bm25mi_kernels.hip)
 };
 SampleGeom sample_geom(int64_t ntiles, int k, int W, int pmax);
+// The geometry a search takes: tile-bound keys when the handle has tile
+// bounds (and the theta_bound option), else sample_geom.  ntiles: the widest
+// shard's tiles (every shard of a search must take the same geometry).
+SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W);
+// Most tiles a shard may have for tile-bound keys (one wave's LDS per query).
+constexpr int64_t kBoundMaxTiles = 30720;
 
 // Kernel launchers (bm25mi_kernels.hip).  All enqueue on `stream`.
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,
                                int32_t* d_err, hipStream_t stream);
+// Tile bounds ix.bmax from the dense segment table and the scores.
+hipError_t launch_build_bmax(const DevIndex& ix, hipStream_t stream);
 // Sparse segment table: non-empty tiles per term -> d_cnt[V] (also writes
 // ldoc and validates, as launch_build_tables), then (after the caller's scan
 // into ix.tl_ptr) the tile lists.

@@ -55,12 +55,14 @@ struct IndexArgs {
   const uint32_t* tl_start;
   const uint64_t* seg;      // sparse + flat kernel: this search's segment table
   int64_t seg_zero;         // ... index of a zero entry past it
+  const uint16_t* bmax;     // dense, non-negative index: f16 upper bound of each (term,
+                            // tile)'s largest score ([V][ntiles]; null: no tile bounds)
 };
 
 static IndexArgs args_of(const DevIndex& ix) {
   return IndexArgs{ix.indptr, ix.rel, ix.ldoc, ix.val, ix.n_terms, ix.ntiles, ix.n_docs,
                    ix.nnz, ix.doc_offset, ix.nonneg ? 1 : 0, ix.sparse ? 1 : 0, ix.tl_ptr,
-                   ix.tl_tile, ix.tl_start, nullptr, 0};
+                   ix.tl_tile, ix.tl_start, nullptr, 0, ix.opt.tile_bound ? ix.bmax : nullptr};
 }
 
 // Segment bounds [r0, r1) (relative to indptr[term]) of a valid term in a
@@ -790,7 +792,15 @@ struct FlatCur {    // XCD-relative item ordinal, its claim's end, band, stage q
 struct FlatDesc {   // lane tile * 2^TL + term: the term's segment in the tile (raw; r1 == r0: none)
   uint32_t ip, r0, r1;
   uint32_t sk;      // REST: score-key half of the tile's best sample key (sample tiles)
+  float bm;         // REST with tile bounds: upper bound of the term's scores in the tile
 };
+
+// f16 bits (of build_bmax_kernel's table) -> float.
+__device__ __forceinline__ float f16_bits_to_float(uint16_t h) {
+  _Float16 x;
+  __builtin_memcpy(&x, &h, 2);
+  return (float)x;
+}
 
 // Row word of the process side: the row's valid positions [lo, hi) of its
 // 128 (position p = lane p / 2, slot p % 2) as lane ranges — slot 0: lanes
@@ -866,7 +876,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const uint64_t* __restrict__ theta, uint64_t* __restrict__ cand, int64_t cstride,
     uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
     int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
-    const uint64_t* __restrict__ skeys, int64_t sstride, int32_t BW, uint64_t* mirror) {
+    const uint64_t* __restrict__ skeys, int64_t sstride, int32_t BW, uint64_t* mirror,
+    int32_t* __restrict__ stats) {
   constexpr int D = 1 << S;
   constexpr int kFR = PH == kSample ? BM25_FR_S : BM25_FR;  // ring slots (>= 2)
   constexpr uint32_t TT = 1u << TL;                          // term lanes per tile
@@ -975,6 +986,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       d.r0 = r[0];
       d.r1 = *(ok ? r + 1 : r);
     }
+    if constexpr (PH == kRest) {  // > the term's largest score in the tile: one f16 step
+      // above its rounded-down maximum (0: outside the item)
+      d.bm = (a.bmax != nullptr && ok)
+                 ? f16_bits_to_float((uint16_t)(a.bmax[tt * a.ntiles + tile] + 1u)) : 0.f;
+    } else {
+      d.bm = 0.f;
+    }
     if (skipping) {  // the score-key half of this tile's best sample key
       // G and P are powers of two (sample_geom): shifts, no integer division
       const uint32_t t32 = (uint32_t)tile;
@@ -990,6 +1008,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     return (uint32_t)(th >> 32) > score_key(0.f);
   };
 
+  uint32_t nbound = 0;  // REST: (query, tile) pairs this lane's tiles skipped by their bound
   // ---- the issue side's item: its segments (lane s = tile * TT + term) and
   // row numbering; the item prefetch pipeline one and two items ahead
   uint32_t iSb = 0, iSl = 0, iIncl = 0, iExcl = 0;
@@ -1004,7 +1023,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const bool th_pos = PH == kRest && th_positive(thN);
     const uint32_t t32 = (uint32_t)(nx.b * BW) + li;  // REST: phase tile = tile
     const bool smp = skipping && ((t32 >> lgG) & (uint32_t)(P - 1)) == 0u;
-    const bool skip = smp && th_pos && dN.sk < (uint32_t)(thN >> 32);
+    bool skip = smp && th_pos && dN.sk < (uint32_t)(thN >> 32);
+    if constexpr (PH == kRest) {
+      // tile bound: no doc of the tile can reach theta when the sum of its
+      // query terms' largest scores in the tile (every term lane of the tile,
+      // duplicates included) is below theta's score.  fp32 addition is
+      // monotone, so the query-order sum of a doc's scores is at most the sum
+      // of these maxima; the 1e-4 margin covers this tree-order sum's own
+      // rounding.  The tile runs no rows and no epilogue.
+      if (a.bmax != nullptr && th_pos) {
+        float ub = dN.bm;
+#pragma unroll
+        for (int o = 1; o < (int)TT; o <<= 1) ub += __shfl_xor(ub, o, 64);
+        const bool cut = ub * 1.0001f < key_score((uint32_t)(thN >> 32));
+        if (cut && !skip && lt == 0u && (int)li < nx.bw) ++nbound;
+        skip = skip || cut;
+      }
+    }
     iSb = dN.ip + dN.r0;
     iSl = skip ? 0u : dN.r1 - dN.r0;
     uint32_t nr = iSl == 0u ? 0u : ((iSb & 1u) + iSl + 127u) >> 7;
@@ -1210,6 +1245,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     for (int s = 0; s < kFR; ++s) step(s);
   }
   if (curTi != kNoTile) epilogue();
+  if (PH == kRest && stats != nullptr) {  // bound-skipped tiles of this wave
+    const uint32_t nb = wave_sum_u32(nbound);
+    if (lane == 0 && nb != 0u) atomicAdd(stats, (int32_t)nb);
+  }
   // every claim of this wave has returned (the last one, read by next(), ran
   // out of items) before it counts itself finished
   finish();
@@ -1389,6 +1428,109 @@ __global__ __launch_bounds__(256) void build_tables_kernel(
       }
     }
   }
+}
+
+// Tile bounds (dense segment table, non-negative index): bmax[t][j] = term
+// t's largest score in tile j as f16 bits rounded down (0: no posting there;
+// 65504 past f16's range), one block per term (coalesced over its tiles), the
+// segments from the rel table.  The value is <= the real maximum (a lower
+// bound: bound_keys_kernel) and the next f16 up is > it (an upper bound: the
+// REST pass's tile skip, inf past the range).
+__global__ __launch_bounds__(256) void build_bmax_kernel(const int64_t* __restrict__ indptr,
+                                                         const uint32_t* __restrict__ rel,
+                                                         const float* __restrict__ val, int64_t V,
+                                                         int64_t ntiles,
+                                                         uint16_t* __restrict__ bmax) {
+  for (int64_t t = blockIdx.x; t < V; t += gridDim.x) {
+    const int64_t ip = indptr[t];
+    const uint32_t* r = rel + t * (ntiles + 1);
+    for (int64_t j = threadIdx.x; j < ntiles; j += blockDim.x) {
+      float m = 0.f;
+      for (int64_t p = ip + r[j]; p < ip + r[j + 1]; ++p) m = fmaxf(m, val[p]);
+      _Float16 h = (_Float16)m;  // round to nearest, then down to <= m
+      uint16_t u;
+      __builtin_memcpy(&u, &h, 2);
+      if ((float)h > m) --u;  // (inf past the range becomes 65504)
+      bmax[t * ntiles + j] = u;
+    }
+  }
+}
+
+// Tile-bound threshold keys (search_geom's P = 0), one wave per query: for
+// every tile j, lb_j = the largest of its query terms' tile maxima (bmax,
+// rounded down).  A document of the tile that holds such a maximum scores at
+// least lb_j — its sum includes that term's score, and fp32 additions of
+// non-negative values never decrease — so the key (lb_j, the tile's LAST
+// doc) is <= that document's own key, and the tiles' keys belong to distinct
+// documents.  The k-th best of them is thus a lower bound of the k-th best
+// key, like the SAMPLE pass's keys, with no posting scored.  Writes this
+// shard's best S keys of every query (global doc ids; 0: fewer positive
+// tiles).  LDS: the tiles' lb_j as f16 bits (ordered as integers: all >= 0).
+__global__ __launch_bounds__(64) void bound_keys_kernel(IndexArgs a,
+                                                        const uint16_t* __restrict__ bmax,
+                                                        const int32_t* __restrict__ queries,
+                                                        int32_t T, int32_t S_log2, int64_t S,
+                                                        uint64_t* __restrict__ keys) {
+  extern __shared__ uint16_t lbv[];
+  const int64_t q = blockIdx.x;
+  const uint32_t lane = lane_id();
+  const int32_t nt = (int32_t)a.ntiles;
+  // the query's terms, 64 at a time one per lane (padding and ids >= V: none)
+  for (int32_t t0 = 0; t0 < T; t0 += 64) {
+    int32_t my = t0 + (int32_t)lane < T ? queries[q * T + t0 + lane] : -1;
+    my = (my >= 0 && (int64_t)my < a.V) ? my : -1;
+    const int32_t nT = min(T - t0, 64);
+    for (int32_t j = (int32_t)lane; j < nt; j += 64) {  // (a lane's own tiles only)
+      uint32_t m = t0 == 0 ? 0u : (uint32_t)lbv[j];
+      for (int i = 0; i < nT; ++i) {
+        const int32_t t = __builtin_amdgcn_readlane(my, i);
+        if (t >= 0) m = max(m, (uint32_t)bmax[(int64_t)t * nt + j]);
+      }
+      lbv[j] = (uint16_t)m;
+    }
+  }
+  if (T <= 0)
+    for (int32_t j = (int32_t)lane; j < nt; j += 64) lbv[j] = 0;
+  __syncthreads();
+  // the k-th largest lb (k = S), bit by bit from the top: a bit of the answer
+  // is set iff at least `need` values match its prefix with that bit set
+  uint32_t v = 0u, need = (uint32_t)S;
+  for (int bit = 15; bit >= 0; --bit) {
+    const uint32_t hm = 0xFFFFu << bit, cand = v | (1u << bit);
+    uint32_t c = 0u;
+    for (int32_t j = (int32_t)lane; j < nt; j += 64) c += ((uint32_t)lbv[j] & hm) == cand;
+    const uint32_t tot = wave_sum_u32(c);
+    if (tot >= need) v = cand;
+    else need -= tot;
+  }
+  // fewer than k positive tiles (v = 0): every positive one, zeros after it.
+  // Otherwise the tiles above v and the first `need` tiles at v (lowest tile
+  // first: their keys are the larger ones), compacted in tile order.
+  uint32_t eq_seen = 0u, kept = 0u;
+  uint64_t* out = keys + q * S;
+  const int32_t nchunk = (nt + 63) >> 6;
+  for (int32_t c = 0; c < nchunk; ++c) {
+    const int32_t j = c * 64 + (int32_t)lane;
+    const uint32_t x = j < nt ? (uint32_t)lbv[j] : 0u;
+    const bool eq = v != 0u && x == v;
+    const uint64_t em = __ballot(eq);
+    const uint32_t erank = eq_seen + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+    const bool keep = x > v || (eq && erank < need);
+    const uint64_t km = __ballot(keep);
+    const uint32_t pos = kept + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
+    if (keep && (int64_t)pos < S) {
+      const int64_t last = min(((int64_t)j + 1) << S_log2, a.n_docs) - 1 + a.doc_offset;
+      _Float16 h;
+      const uint16_t xb = (uint16_t)x;
+      __builtin_memcpy(&h, &xb, 2);
+      out[pos] = ((uint64_t)score_key((float)h) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)last);
+    }
+    eq_seen += (uint32_t)__popcll(em);
+    kept += (uint32_t)__popcll(km);
+  }
+  for (int64_t p = (int64_t)kept + lane; p < S; p += 64) out[p] = 0ull;
 }
 
 // Sparse segment table, pass 1: ldoc + validation (as build_tables_kernel)
@@ -2086,6 +2228,14 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
   return hipGetLastError();
 }
 
+hipError_t launch_build_bmax(const DevIndex& ix, hipStream_t stream) {
+  if (ix.n_terms == 0 || ix.ntiles == 0 || !ix.bmax || ix.sparse) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>(ix.n_terms, 65536);
+  hipLaunchKernelGGL(build_bmax_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, ix.indptr,
+                     ix.rel, ix.val, ix.n_terms, ix.ntiles, ix.bmax);
+  return hipGetLastError();
+}
+
 hipError_t launch_count_tiles(const DevIndex& ix, const int32_t* d_indices, int64_t* d_cnt,
                               int32_t* d_err, hipStream_t stream) {
   if (ix.n_terms == 0) return hipSuccess;
@@ -2120,6 +2270,19 @@ SampleGeom sample_geom(int64_t ntiles, int k, int W, int pmax) {
       if (nS * m * W >= 2 * (int64_t)k) return SampleGeom{P, m, nS * m, G};
   }
   return SampleGeom{1, 0, 0, 1};
+}
+
+// Tile-bound keys (P = 0) need the tile bounds (a dense, non-negative index
+// with its bmax table; an empty shard contributes no keys either way), at
+// most kBoundMaxTiles tiles and a collection of at least 2k tiles (one key
+// per tile); otherwise the SAMPLE pass (sample_geom).  sample_p = 1 keeps
+// asking for the exact pass.
+SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W) {
+  const bool bounds = ix.ntiles == 0 || (ix.bmax != nullptr && ix.nonneg && !ix.sparse);
+  if (ix.opt.theta_bound && ix.opt.sample_p > 1 && bounds && k >= 1 && ntiles <= kBoundMaxTiles &&
+      ntiles * std::max(W, 1) >= 2 * (int64_t)k)
+    return SampleGeom{0, 1, (int64_t)k, 1};
+  return sample_geom(ntiles, k, W, ix.opt.sample_p);
 }
 
 // Every resident workgroup slot of the current device (a multiple of 8, one
@@ -2192,7 +2355,8 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
                        sg.G, sg.nq_host, sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, sg.cstride,
                        ws.list, ws.list_cnt, ws.list_cap, wctr, ix.opt.claim_ch, claim_m,
                        skip ? sg.sample_keys : nullptr, sg.sample_stride, bw,
-                       PH == kSample && SM == 1 ? sg.cand_mirror : nullptr);
+                       PH == kSample && SM == 1 ? sg.cand_mirror : nullptr,
+                       PH == kRest ? ws.counters + 5 : nullptr);
   };
   if (ix.sparse)
     go(score_flat_kernel<S, PH, SM, true, TL>);
@@ -2299,8 +2463,8 @@ static void launch_seg_table(const DevIndex& ix, const int32_t* q, int64_t Q, in
                      args_of(ix), q, Q, (int32_t)T, (int32_t)flat_term_lanes(T), ws.seg);
 }
 
-// P > 1: the sampled search (its merge reads the list only: nt = 0);
-// P = 1: the exact path over every tile.
+// P != 1: the thresholded search (sampled, or tile-bound keys at P = 0; its
+// merge reads the list only: nt = 0); P = 1: the exact path over every tile.
 static Stage main_stage(const DevIndex& ix, int64_t Q, int P, const Workspace& ws) {
   Stage sg{};
   sg.cand = ws.cand;
@@ -2308,9 +2472,9 @@ static Stage main_stage(const DevIndex& ix, int64_t Q, int P, const Workspace& w
   sg.cstride = ix.ntiles * kTileM;
   sg.P = P;
   sg.G = 1;
-  sg.nt = P > 1 ? 0 : ix.ntiles;
+  sg.nt = P != 1 ? 0 : ix.ntiles;
   sg.nq_host = (int32_t)Q;
-  if (P > 1) {
+  if (P != 1) {
     sg.theta = ws.theta;
     sg.list = ws.list;
     sg.list_cnt = ws.list_cnt;
@@ -2374,8 +2538,10 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
   sg.ctr_region = 1;  // counters and list counts: reset by theta_wave_kernel
   sg.M = g.m;
   sg.G = g.G;
-  sg.sample_keys = ws.cand;  // launch_sample left this shard's keys there
-  sg.sample_stride = g.S;
+  if (g.P > 1) {  // the sample tiles' keys: launch_sample left this shard's copy there
+    sg.sample_keys = ws.cand;
+    sg.sample_stride = g.S;
+  }
   hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, st, all_keys,
                      (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap,
                      ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs, ws.counters);
@@ -2396,6 +2562,16 @@ hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q
     hipMemsetAsync(keys, 0, sizeof(uint64_t) * Q * g.S, stream);
     return hipGetLastError();
   }
+  if (g.P == 0) {  // tile-bound keys: no posting is scored before REST
+    if (ix.bmax == nullptr || ix.ntiles > kBoundMaxTiles || Q > 0x7FFFFFFF)
+      return hipErrorInvalidValue;
+    if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, d_queries, Q, T, ws, stream);
+    ix.disp.kernels |= kKBound;
+    hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(64),
+                       (size_t)((ix.ntiles * 2 + 15) & ~15ll), stream, args_of(ix), ix.bmax,
+                       d_queries, (int32_t)T, ix.tile_shift, g.S, keys);
+    return hipGetLastError();
+  }
 #define CALL(s) sample_s<s>(ix, d_queries, Q, T, g, keys, ws, stream)
   BM25_SHIFT_DISPATCH(CALL)
 #undef CALL
@@ -2414,7 +2590,7 @@ hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q
 
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                         int k, const Workspace& ws, hipStream_t stream) {
-  const SampleGeom g = sample_geom(ix.ntiles, k, 1, ix.opt.sample_p);
+  const SampleGeom g = search_geom(ix, ix.ntiles, k, 1);
   hipError_t e = launch_sample(ix, d_queries, Q, T, g, ws.cand, ws, stream);
   if (e != hipSuccess) return e;
   return launch_finish(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream);

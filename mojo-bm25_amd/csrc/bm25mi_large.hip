@@ -96,19 +96,47 @@ __global__ __launch_bounds__(256) void lk_hist_kernel(const float* __restrict__ 
   const float4* row = reinterpret_cast<const float4*>(scores + g * stride);
   const int64_t n4 = (n_docs + 3) >> 2;
   uint32_t zeros = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const float4 f = row[i];
-    const float fe[4] = {f.x, f.y, f.z, f.w};
+  const uint32_t lane = threadIdx.x & 63u;
+  // every lane of a wave runs the same rounds (the ballots below)
+  const int64_t step = (int64_t)gridDim.x * 256;
+  const int64_t rounds = (n4 + step - 1) / step;
+  for (int64_t r = 0; r < rounds; ++r) {
+    const int64_t i = r * step + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    float fe[4] = {0.f, 0.f, 0.f, 0.f};
+    if (i < n4) {
+      const float4 f = row[i];
+      fe[0] = f.x;
+      fe[1] = f.y;
+      fe[2] = f.z;
+      fe[3] = f.w;
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int64_t d = 4 * i + c;
-      if (d >= n_docs) break;
-      if (zfast && __float_as_uint(fe[c]) == 0u) {
+      bool pend = d < n_docs;
+      if (pend && zfast && __float_as_uint(fe[c]) == 0u) {
         zeros += zmatch ? 1u : 0u;
-        continue;
+        pend = false;
       }
       const uint64_t key = doc_key(fe[c], (uint32_t)d);
-      if (match(key)) atomicAdd(&h[(uint32_t)(key >> shift) & 255u], 1u);
+      pend = pend && match(key);
+      const uint32_t dig = (uint32_t)(key >> shift) & 255u;
+      // the high digits of a row's scores are few (one exponent range): the
+      // lanes that share the first pending lane's digit add once, twice over,
+      // and the rest (distinct digits, no same-address serialisation) add
+      // one by one
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const uint64_t m = __ballot(pend);
+        if (m == 0ull) break;  // wave-uniform
+        const int leader = __builtin_ctzll(m);
+        const uint32_t dl = (uint32_t)__shfl((int)dig, leader, 64);
+        const bool same = pend && dig == dl;
+        const uint64_t sm = __ballot(same);
+        if ((int)lane == leader) atomicAdd(&h[dl], (uint32_t)__popcll(sm));
+        pend = pend && !same;
+      }
+      if (pend) atomicAdd(&h[dig], 1u);
     }
   }
   zeros = wave_sum(zeros);

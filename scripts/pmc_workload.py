@@ -20,6 +20,9 @@ ap.add_argument("--searches", type=int, default=5)
 args = ap.parse_args()
 
 import torch  # noqa: E402
+if os.environ.get("VLIB"):  # a variant build (scripts/build_variant.sh)
+    import importlib  # (bm25mi.build as an attribute is the build() function)
+    importlib.import_module("bm25mi.build").LIB = os.path.abspath(os.environ["VLIB"])
 from bm25mi import synth  # noqa: E402
 from bm25mi.index import GpuIndex  # noqa: E402
 

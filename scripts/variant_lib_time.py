@@ -38,9 +38,13 @@ for _ in range(20):
 p = index.profile_read()
 torch.cuda.synchronize()
 h = int((d.to(torch.int64) * 1000003 + s.view(torch.int32).to(torch.int64)).sum().item())
+ss = index.search_stats()
 print(json.dumps({"lib": os.path.basename(_capi.LIB), "env": os.environ.get("VENV", ""),
                   "cfg": os.environ.get("VCFG", "c3"), "terms": cfg.terms_per_query, "score_ms": round(p["score_ms"] / p["score_launches"], 4),
-                  "total_ms": round(p["total_ms"] / p["searches"], 4), "hash": h}), flush=True)
+                  "total_ms": round(p["total_ms"] / p["searches"], 4), "hash": h,
+                  "kernels": sorted(index.last_dispatch()["kernels"]),
+                  "fallback_queries": ss["fallback_queries"],
+                  "bound_skipped_tiles": ss["bound_skipped_tiles"]}), flush=True)
 '''
 for arg in sys.argv[1:]:  # LIB[:NAME=VAL,NAME=VAL]: per-library environment
     lib, _, kv = arg.partition(":")

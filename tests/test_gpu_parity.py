@@ -1015,3 +1015,137 @@ def test_rccl_all_gather_branch(gpu):
         assert tuple(kk.shape) == (1, 5, 3) and int(kk[0, 4, 2]) == 14
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("T", [4, 12])
+def test_tile_bound_skips_exact(gpu, T):
+    """The REST pass skips the (query, tile) pairs whose query-term maxima
+    (f16 upper bounds per (term, tile)) sum below the threshold: same bits
+    with and without (tile_bound option), and tiles are actually skipped —
+    rare high-scoring terms (present in few tiles) beside common low-scoring
+    ones, ties at the threshold from quarter-step values."""
+    rng = np.random.default_rng(50 + T)
+    N, V = 3_000_000, 400
+    indptr, idx, dat = [0], [], []
+    for t in range(V):
+        df = int(rng.integers(200_000, 900_000)) if t < 40 else int(rng.integers(5, 400))
+        idx.append(np.sort(rng.choice(N, df, replace=False)).astype(np.int32))
+        hi = 1.0 if t < 40 else 9.0
+        dat.append((np.round(rng.uniform(0.1, hi, df) * 4) / 4 + 0.25).astype(np.float32))
+        indptr.append(indptr[-1] + df)
+    ip, ix, dt = np.array(indptr, np.int64), np.concatenate(idx), np.concatenate(dat)
+    q = np.concatenate([rng.integers(0, 40, size=(48, T // 2)),
+                        rng.integers(40, V, size=(48, T - T // 2))], axis=1).astype(np.int32)
+    q[0, :] = -1
+    q[1, 1:] = q[1, 0]
+    index = _idx(ip, ix, dt, N, segments="dense")
+    assert index.get_option("tile_bound") == 1
+    for k in (10, 100):
+        ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
+        _exact(index.search(q, k), ref)
+        skipped = index.search_stats()["bound_skipped_tiles"]
+        assert skipped > 0, skipped
+        index.set_option("tile_bound", 0)
+        _exact(index.search(q, k), ref)
+        assert index.search_stats()["bound_skipped_tiles"] == 0
+        index.set_option("tile_bound", 1)
+
+
+def _bound_case(seed, N, V, heavy, big=False):
+    """CSC with `heavy` common low-scoring terms and rare high-scoring ones
+    (quarter-step values: ties); big: also scores past f16's range and below
+    its smallest subnormal (the rounding edges of the tile bounds)."""
+    rng = np.random.default_rng(seed)
+    indptr, idx, dat = [0], [], []
+    for t in range(V):
+        df = int(rng.integers(N // 15, N // 4)) if t < heavy else int(rng.integers(1, 300))
+        idx.append(np.sort(rng.choice(N, df, replace=False)).astype(np.int32))
+        hi = 1.0 if t < heavy else 9.0
+        v = (np.round(rng.uniform(0.1, hi, df) * 4) / 4 + 0.25).astype(np.float32)
+        if big and t % 7 == 3:
+            v[::3] = np.float32(70000.0) + np.float32(t)
+        if big and t % 7 == 5:
+            v[::2] = np.float32(1e-30)
+        dat.append(v)
+        indptr.append(indptr[-1] + df)
+    return np.array(indptr, np.int64), np.concatenate(idx), np.concatenate(dat)
+
+
+@pytest.mark.parametrize("T,big", [(4, False), (12, False), (9, True), (70, False)])
+def test_theta_bound_exact(gpu, T, big):
+    """Threshold keys from the tile bounds (theta_bound, no SAMPLE pass): the
+    same bits as the sampled threshold and as the oracle, with and without
+    the REST tile skip — ties at the threshold (quarter-step values), rows
+    with fewer positive tiles than k (zero-fill), padding, duplicates, ids
+    >= V, scores past f16's range and below its subnormals, and T > 64 (the
+    wave kernel's REST)."""
+    N, V = 1_500_000, 300
+    ip, ix, dt = _bound_case(70 + T, N, V, 30, big)
+    rng = np.random.default_rng(T)
+    q = np.concatenate([rng.integers(0, 30, size=(40, T // 2)),
+                        rng.integers(30, V, size=(40, T - T // 2))], axis=1).astype(np.int32)
+    q[0, :] = -1
+    q[1, 1:] = q[1, 0]
+    q[2, :] = -1
+    q[2, 0] = 30 + int(np.argmin(np.diff(ip)[30:]))  # one rare term: < k positive tiles
+    q[3, -1] = V + 5
+    index = _idx(ip, ix, dt, N, segments="dense")
+    assert index.get_option("theta_bound") == 1
+    for k in (1, 10, 100):
+        ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
+        for tb in (1, 0):
+            for tl in (1, 0):
+                index.set_option("theta_bound", tb)
+                index.set_option("tile_bound", tl)
+                _exact(index.search(q, k), ref)
+                d = index.last_dispatch()
+                assert ("bound_keys" in d["kernels"]) == bool(tb), (tb, d)
+                assert (d["sample_p"] == 0) == bool(tb), d
+    index.set_option("theta_bound", 1)
+    index.set_option("tile_bound", 1)
+    index.close()
+
+
+def test_theta_bound_sharded_protocol(gpu):
+    """The two-half sharded protocol with tile-bound keys: S = k per shard,
+    every shard's best k keys all-gathered (here: stacked on one GPU), the
+    world's k-th key as theta, lists merged — bit-exact vs the single-index
+    oracle, also with one empty-ish shard and k above a shard's tiles."""
+    import torch
+    from bm25mi.index import merge_topk_device
+    N, V = 600_000, 200
+    ip, ix, dt = _bound_case(91, N, V, 20)
+    rng = np.random.default_rng(5)
+    q = np.concatenate([rng.integers(0, 20, size=(24, 3)),
+                        rng.integers(20, V, size=(24, 3))], axis=1).astype(np.int32)
+    cuts = [0, 2048 * 40, 2048 * 200, N]
+    import scipy.sparse as sp
+    m = sp.csc_matrix((dt, ix, ip), shape=(N, V))
+    shards = []
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        s = m[lo:hi].tocsc()
+        s.sort_indices()
+        shards.append(_idx(s.indptr.astype(np.int64), s.indices.astype(np.int32),
+                           s.data.astype(np.float32), hi - lo, doc_offset=lo, segments="dense"))
+    W = len(shards)
+    smax = max(hi - lo for lo, hi in zip(cuts[:-1], cuts[1:]))
+    dq = torch.from_numpy(q).cuda()
+    for k in (10, 100):
+        S = shards[0].sample_width(k, W, smax)
+        assert S == k, S
+        keys = torch.zeros((W, q.shape[0], S), dtype=torch.int64, device="cuda")
+        for r, s in enumerate(shards):
+            s.search_sample_device(dq, k, W, smax, keys[r])
+        d = torch.empty((W, q.shape[0], k), dtype=torch.int32, device="cuda")
+        sc = torch.empty((W, q.shape[0], k), dtype=torch.float32, device="cuda")
+        for r, s in enumerate(shards):
+            s.search_finish_device(dq, k, W, smax, keys, d[r], sc[r])
+            assert "bound_keys" in s.last_dispatch()["kernels"]
+        od = torch.empty((q.shape[0], k), dtype=torch.int32, device="cuda")
+        os_ = torch.empty((q.shape[0], k), dtype=torch.float32, device="cuda")
+        merge_topk_device(0, d, sc, W, q.shape[0], k, od, os_)
+        torch.cuda.synchronize()
+        ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
+        _exact((od.cpu().numpy(), os_.cpu().numpy()), ref)
+    for s in shards:
+        s.close()
