@@ -94,6 +94,14 @@ int bm25_index_info(const bm25_index* idx, int64_t* n_docs, int64_t* n_terms,
 int bm25_index_segments(const bm25_index* idx, int32_t* sparse, int64_t* n_pairs);
 
 /*
+ * Tile bounds of a built index: *has_bounds = 1 when it keeps
+ * each (term, tile)'s largest score (a dense, non-negative index whose table
+ * fit in device memory) — the tile-bound threshold and the REST tile skip
+ * need it; *bytes = the table's device bytes.  Any pointer may be NULL.
+ */
+int bm25_index_bounds(const bm25_index* idx, int32_t* has_bounds, int64_t* bytes);
+
+/*
  * Batched top-k search, host buffers, synchronous.
  * Replaces: BM25v.search / get_scores / _compute_relevance_from_scores / _topk
  *           (bm25_native.py:76-158, 204-214).
@@ -199,8 +207,8 @@ int bm25_merge_sorted_device(int device, const int32_t* d_docs,
  *   bm25_sample_width(idx, shard_docs_max, world, k, &S): keys per query each
  *     rank samples (the same on every rank: shard_docs_max = the largest
  *     shard's document count; S = 0: shards too small to sample, or
- *     k > 4096 — then the finish half lists the shard's exact top-k; S = k
- *     with the theta_bound option: tile-bound keys);
+ *     k > 4096 — then the finish half lists the shard's exact top-k; S =
+ *     min(k, ceil(2k / world)) tile-bound keys with the theta_bound option);
  *   bm25_search_sample_device(...): this shard's sample keys -> d_keys
  *     (u64 [Q][S], zero-padded: a SAMPLE pass, or — theta_bound — the best S
  *     tile-bound keys, read from the tile bounds without scoring);

@@ -52,6 +52,7 @@ _SIGS = {
     "bm25_index_destroy": ([_P], ctypes.c_int),
     "bm25_index_info": ([_P, _PI64, _PI64, _PI64, _PI32, _PI64, _PI64], ctypes.c_int),
     "bm25_index_segments": ([_P, _PI32, _PI64], ctypes.c_int),
+    "bm25_index_bounds": ([_P, _PI32, _PI64], ctypes.c_int),
     "bm25_search": ([_P, _P, _I64, _I64, _I32, _P, _P], ctypes.c_int),
     "bm25_search_device": ([_P, _P, _I64, _I64, _I32, _P, _P, _P], ctypes.c_int),
     "bm25_max_token_device": ([_P, _P, _I64, _I64, _P, _P], ctypes.c_int),

@@ -91,9 +91,13 @@ class GpuIndex:
         sp_ = ctypes.c_int32()
         npairs = ctypes.c_int64()
         check(lib.bm25_index_segments(self._h, ctypes.byref(sp_), ctypes.byref(npairs)))
+        hb = ctypes.c_int32()
+        bb = ctypes.c_int64()
+        check(lib.bm25_index_bounds(self._h, ctypes.byref(hb), ctypes.byref(bb)))
         return {"n_docs": vals[0].value, "n_terms": vals[1].value, "nnz": vals[2].value,
                 "tile_docs": td.value, "n_tiles": nt.value, "device_bytes": db.value,
-                "sparse": bool(sp_.value), "n_pairs": npairs.value}
+                "sparse": bool(sp_.value), "n_pairs": npairs.value,
+                "tile_bounds": bool(hb.value), "tile_bound_bytes": bb.value}
 
     # ------------------------------------------------------------------
     def search(self, queries: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:

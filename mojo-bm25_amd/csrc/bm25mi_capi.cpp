@@ -307,7 +307,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   int rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
-  const int P = search_geom(h->ix, h->ix.ntiles, k, 1).P;
+  const int P = search_geom(h->ix, h->ix.ntiles, k, 1, T).P;
   h->ix.disp = Dispatch{};
   h->ix.disp.sample_p = P;
   EventPair* ev = next_events(h);
@@ -555,6 +555,14 @@ int bm25_index_segments(const bm25_index* h, int32_t* sparse, int64_t* n_pairs) 
   return BM25_OK;
 }
 
+int bm25_index_bounds(const bm25_index* h, int32_t* has_bounds, int64_t* bytes) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  const bool on = h->ix.bmax != nullptr;
+  if (has_bounds) *has_bounds = on ? 1 : 0;
+  if (bytes) *bytes = on ? (int64_t)sizeof(uint16_t) * h->ix.n_terms * h->ix.ntiles : 0;
+  return BM25_OK;
+}
+
 int bm25_search(bm25_index* h, const int32_t* queries, int64_t Q, int64_t T, int32_t k,
                 int32_t* out_docs, float* out_scores) {
   if (!h) return fail(BM25_EINVAL, "NULL index");
@@ -614,10 +622,12 @@ int bm25_max_token_device(bm25_index* h, const int32_t* d_queries, int64_t Q, in
 }
 
 // Two-phase search of W doc shards with a global threshold (bm25mi.h).
-static SampleGeom shard_geom(const bm25_index* h, int64_t shard_docs_max, int32_t world, int k) {
+// (T = 0: the width alone — the same for every T, search_geom)
+static SampleGeom shard_geom(const bm25_index* h, int64_t shard_docs_max, int32_t world, int k,
+                             int64_t T = 0) {
   const int64_t D = 1ll << h->ix.tile_shift;
   const int64_t nt = std::max<int64_t>((std::max<int64_t>(shard_docs_max, h->ix.n_docs) + D - 1) / D, 1);
-  return search_geom(h->ix, nt, k, std::max(world, 1));
+  return search_geom(h->ix, nt, k, std::max(world, 1), T);
 }
 
 int bm25_sample_width(const bm25_index* h, int64_t shard_docs_max, int32_t world, int32_t k,
@@ -645,7 +655,7 @@ int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   HIP_TRY(order_ws(h, st), "workspace order");
   h->split_ev = next_events(h);
   if (h->split_ev) HIP_TRY(hipEventRecord(h->split_ev->a, st), "hipEventRecord");
-  const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
+  const SampleGeom g = shard_geom(h, shard_docs_max, world, k, T);
   h->ix.disp = Dispatch{};
   h->ix.disp.sample_p = g.P;
   h->sampled = true;
@@ -672,7 +682,7 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
-  const SampleGeom g = shard_geom(h, shard_docs_max, world, k);
+  const SampleGeom g = shard_geom(h, shard_docs_max, world, k, T);
   if (!h->sampled) {  // no sample half ran for this search (S = 0)
     h->ix.disp = Dispatch{};
     h->ix.disp.sample_p = g.P;

@@ -159,7 +159,7 @@ inline int64_t maxflag_for(int k, int64_t ntiles) {
 // Threshold geometry of a search over W doc shards of ntiles tiles each:
 // stride P (1 = no sampling), m keys per sample tile, S keys per query per
 // shard, sample tiles in groups of G consecutive tiles (one group per G*P).
-// P = 0: no SAMPLE pass — each shard's S = k best tile-bound keys
+// P = 0: no SAMPLE pass — each shard's S best tile-bound keys
 // (bound_keys_kernel).
 struct SampleGeom {
   int P, m;
@@ -167,12 +167,18 @@ struct SampleGeom {
   int G;  // sample tiles come in groups of G consecutive tiles (bm25mi_kernels.hip)
 };
 SampleGeom sample_geom(int64_t ntiles, int k, int W, int pmax);
-// The geometry a search takes: tile-bound keys when the handle has tile
-// bounds (and the theta_bound option), else sample_geom.  ntiles: the widest
-// shard's tiles (every shard of a search must take the same geometry).
-SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W);
+// The geometry a search of T-term queries takes: tile-bound keys when the
+// handle has tile bounds (and the theta_bound option) and the queries are
+// short, else sample_geom; the key width S is sample_geom's either way.
+// ntiles: the widest shard's tiles (every shard of a search must take the
+// same geometry).
+SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W, int64_t T);
 // Most tiles a shard may have for tile-bound keys (one wave's LDS per query).
 constexpr int64_t kBoundMaxTiles = 30720;
+// ... and at least this many tiles per wanted key over the whole collection.
+constexpr int64_t kBoundTilesPerK = 16;
+// ... and queries of at most this many terms (search_geom).
+constexpr int64_t kBoundMaxTerms = 8;
 
 // Kernel launchers (bm25mi_kernels.hip).  All enqueue on `stream`.
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,

@@ -791,8 +791,10 @@ struct FlatCur {    // XCD-relative item ordinal, its claim's end, band, stage q
 
 struct FlatDesc {   // lane tile * 2^TL + term: the term's segment in the tile (raw; r1 == r0: none)
   uint32_t ip, r0, r1;
-  uint32_t sk;      // REST: score-key half of the tile's best sample key (sample tiles)
-  float bm;         // REST with tile bounds: upper bound of the term's scores in the tile
+  uint32_t aux;     // REST, one of (the launch never asks for both):
+                    //   tile bounds: f16 bits of an upper bound of the term's scores in
+                    //     the tile (one step above bmax; 0 outside the item)
+                    //   sample skip: score-key half of the tile's best sample key
 };
 
 // f16 bits (of build_bmax_kernel's table) -> float.
@@ -961,7 +963,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   };
   // REST: sample tiles (groups of G = kSampleGroup tiles, one group per G * P)
   // whose best sample key is below theta are skipped
-  const bool skipping = PH == kRest && skeys != nullptr && G == kSampleGroup;
+  const bool skipping = PH == kRest && skeys != nullptr && G == kSampleGroup && a.bmax == nullptr;
   const uint32_t lgG = (uint32_t)__builtin_ctz((unsigned)G), lgP = (uint32_t)__builtin_ctz((unsigned)P);
   // an item's segment descriptors (4 VGPRs: a lane outside the item reads its
   // r1 from r0's address, so r1 - r0 = 0 needs no flag; the sample-tile test
@@ -986,21 +988,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       d.r0 = r[0];
       d.r1 = *(ok ? r + 1 : r);
     }
-    if constexpr (PH == kRest) {  // > the term's largest score in the tile: one f16 step
-      // above its rounded-down maximum (0: outside the item)
-      d.bm = (a.bmax != nullptr && ok)
-                 ? f16_bits_to_float((uint16_t)(a.bmax[tt * a.ntiles + tile] + 1u)) : 0.f;
-    } else {
-      d.bm = 0.f;
-    }
-    if (skipping) {  // the score-key half of this tile's best sample key
+    d.aux = 0u;
+    if (PH == kRest && a.bmax != nullptr) {  // > the term's largest score in the tile: one
+      // f16 step above its rounded-down maximum
+      if (ok) d.aux = (uint32_t)a.bmax[tt * a.ntiles + tile] + 1u;
+    } else if (skipping) {  // the score-key half of this tile's best sample key
       // G and P are powers of two (sample_geom): shifts, no integer division
       const uint32_t t32 = (uint32_t)tile;
       const int64_t si = (int64_t)(((t32 >> (lgG + lgP)) << lgG) | (t32 & (uint32_t)(G - 1)));
-      d.sk = reinterpret_cast<const uint32_t*>(skeys)[2 * ((int64_t)c.q * sstride +
-                                                             min<int64_t>(si, sstride - 1)) + 1];
-    } else {
-      d.sk = 0u;
+      d.aux = reinterpret_cast<const uint32_t*>(skeys)[2 * ((int64_t)c.q * sstride +
+                                                              min<int64_t>(si, sstride - 1)) + 1];
     }
     return d;
   };
@@ -1023,7 +1020,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const bool th_pos = PH == kRest && th_positive(thN);
     const uint32_t t32 = (uint32_t)(nx.b * BW) + li;  // REST: phase tile = tile
     const bool smp = skipping && ((t32 >> lgG) & (uint32_t)(P - 1)) == 0u;
-    bool skip = smp && th_pos && dN.sk < (uint32_t)(thN >> 32);
+    bool skip = smp && th_pos && dN.aux < (uint32_t)(thN >> 32);
     if constexpr (PH == kRest) {
       // tile bound: no doc of the tile can reach theta when the sum of its
       // query terms' largest scores in the tile (every term lane of the tile,
@@ -1032,7 +1029,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       // of these maxima; the 1e-4 margin covers this tree-order sum's own
       // rounding.  The tile runs no rows and no epilogue.
       if (a.bmax != nullptr && th_pos) {
-        float ub = dN.bm;
+        float ub = f16_bits_to_float((uint16_t)dN.aux);
 #pragma unroll
         for (int o = 1; o < (int)TT; o <<= 1) ub += __shfl_xor(ub, o, 64);
         const bool cut = ub * 1.0001f < key_score((uint32_t)(thN >> 32));
@@ -1475,22 +1472,18 @@ __global__ __launch_bounds__(64) void bound_keys_kernel(IndexArgs a,
   const int64_t q = blockIdx.x;
   const uint32_t lane = lane_id();
   const int32_t nt = (int32_t)a.ntiles;
-  // the query's terms, 64 at a time one per lane (padding and ids >= V: none)
-  for (int32_t t0 = 0; t0 < T; t0 += 64) {
-    int32_t my = t0 + (int32_t)lane < T ? queries[q * T + t0 + lane] : -1;
-    my = (my >= 0 && (int64_t)my < a.V) ? my : -1;
-    const int32_t nT = min(T - t0, 64);
-    for (int32_t j = (int32_t)lane; j < nt; j += 64) {  // (a lane's own tiles only)
-      uint32_t m = t0 == 0 ? 0u : (uint32_t)lbv[j];
-      for (int i = 0; i < nT; ++i) {
-        const int32_t t = __builtin_amdgcn_readlane(my, i);
-        if (t >= 0) m = max(m, (uint32_t)bmax[(int64_t)t * nt + j]);
-      }
-      lbv[j] = (uint16_t)m;
+  // the query's terms as scalar loads (uniform addresses; padding and ids
+  // >= V: none).  Not a readlane of a per-lane copy: the compiler may compute
+  // that copy only in the lanes of the divergent tile loop that uses it.
+  const int32_t* qt = queries + q * T;
+  for (int32_t j = (int32_t)lane; j < nt; j += 64) {  // (a lane's own tiles only)
+    uint32_t m = 0u;
+    for (int32_t i = 0; i < T; ++i) {
+      const int32_t t = __builtin_amdgcn_readfirstlane(qt[i]);
+      if (t >= 0 && (int64_t)t < a.V) m = max(m, (uint32_t)bmax[(int64_t)t * nt + j]);
     }
+    lbv[j] = (uint16_t)m;
   }
-  if (T <= 0)
-    for (int32_t j = (int32_t)lane; j < nt; j += 64) lbv[j] = 0;
   __syncthreads();
   // the k-th largest lb (k = S), bit by bit from the top: a bit of the answer
   // is set iff at least `need` values match its prefix with that bit set
@@ -2274,15 +2267,26 @@ SampleGeom sample_geom(int64_t ntiles, int k, int W, int pmax) {
 
 // Tile-bound keys (P = 0) need the tile bounds (a dense, non-negative index
 // with its bmax table; an empty shard contributes no keys either way), at
-// most kBoundMaxTiles tiles and a collection of at least 2k tiles (one key
-// per tile); otherwise the SAMPLE pass (sample_geom).  sample_p = 1 keeps
-// asking for the exact pass.
-SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W) {
+// most kBoundMaxTiles tiles, a collection of at least kBoundTilesPerK * k
+// tiles — one key per tile, and the k-th best single-term maximum is only a
+// tight threshold while k is a small share of the tiles (at k ~ tiles / 2
+// every query's list overflows) — and queries of at most kBoundMaxTerms
+// terms: a longer query's sum of many terms lies further above its largest
+// single-term score, and its SAMPLE pass pays for itself (measured: 16-term
+// queries at config 3 take 5.34 ms sampled, 5.62 with tile-bound keys).
+// Otherwise the SAMPLE pass (sample_geom), whose sample tiles report up to
+// 4 real sums each; sample_p = 1 keeps asking for the exact pass.  The key
+// width S is the sampled geometry's either way (so bm25_sample_width needs no
+// T): any set of such keys of distinct documents gives a valid theta (the
+// k-th best of them), and each shard's best S (W * S >= 2k) are the world's
+// k best unless a shard holds more than S of them.
+SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W, int64_t T) {
+  const SampleGeom g = sample_geom(ntiles, k, W, ix.opt.sample_p);
   const bool bounds = ix.ntiles == 0 || (ix.bmax != nullptr && ix.nonneg && !ix.sparse);
-  if (ix.opt.theta_bound && ix.opt.sample_p > 1 && bounds && k >= 1 && ntiles <= kBoundMaxTiles &&
-      ntiles * std::max(W, 1) >= 2 * (int64_t)k)
-    return SampleGeom{0, 1, (int64_t)k, 1};
-  return sample_geom(ntiles, k, W, ix.opt.sample_p);
+  if (g.P > 1 && ix.opt.theta_bound && bounds && k >= 1 && T >= 1 && T <= kBoundMaxTerms &&
+      ntiles <= kBoundMaxTiles && ntiles * std::max(W, 1) >= kBoundTilesPerK * (int64_t)k)
+    return SampleGeom{0, 1, g.S, 1};
+  return g;
 }
 
 // Every resident workgroup slot of the current device (a multiple of 8, one
@@ -2338,6 +2342,7 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
   // in groups of 8 tiles: ws.cand holds this shard's sample keys)
   const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kSampleGroup;
   IndexArgs a = args_of(ix);
+  if (skip) a.bmax = nullptr;  // one descriptor field: the sample keys' skip or the tile bounds
   a.seg = ws.seg;
   a.seg_zero = Qb * ((ix.ntiles + 7) >> 3) * 8 * (1 << TL);
   const int64_t nt = PH == kSample ? sample_count(ix.ntiles, sg.P, sg.G) : ix.ntiles;
@@ -2590,7 +2595,7 @@ hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q
 
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                         int k, const Workspace& ws, hipStream_t stream) {
-  const SampleGeom g = search_geom(ix, ix.ntiles, k, 1);
+  const SampleGeom g = search_geom(ix, ix.ntiles, k, 1, T);
   hipError_t e = launch_sample(ix, d_queries, Q, T, g, ws.cand, ws, stream);
   if (e != hipSuccess) return e;
   return launch_finish(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream);

@@ -39,6 +39,17 @@ def _idx(indptr, indices, data, n_docs, doc_offset=0, segments=None, options=Non
 # which reads its query count on the device), or one exact ALL pass
 FLAT_SAMPLED = {"flat_sample", "flat_rest", "flat_all"}
 WAVE_SAMPLED = {"wave_sample", "wave_rest", "wave_all"}
+FLAT_BOUND = {"bound_keys", "flat_rest", "flat_all"}
+WAVE_BOUND = {"bound_keys", "wave_rest", "wave_all"}
+
+
+def _want_kernels(P, flat=True):
+    """The score kernels a search of threshold geometry P launches."""
+    if P == 1:
+        return {"flat_all" if flat else "wave_all"}
+    if P == 0:
+        return FLAT_BOUND if flat else WAVE_BOUND
+    return FLAT_SAMPLED if flat else WAVE_SAMPLED
 
 
 def _progress(msg):
@@ -196,10 +207,10 @@ def test_flat_kernel_query_widths(gpu, T, lanes, segments):
     for k in (1, 25, 300):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
         d = index.last_dispatch()
-        sampled = _sample_p(index.info()["n_tiles"], k) > 1
-        assert d["kernels"] == (FLAT_SAMPLED if sampled else {"flat_all"}), d
+        P = _geom_p(index, k, T=T)
+        assert d["kernels"] == _want_kernels(P) and d["sample_p"] == P, d
         assert d["term_lanes"] == lanes, d
-        assert 1 <= d["band_tiles"]["rest" if sampled else "all"] <= 64 // lanes
+        assert 1 <= d["band_tiles"]["rest" if P != 1 else "all"] <= 64 // lanes
 
 
 @pytest.mark.parametrize("T", [0, 65, 80])
@@ -216,8 +227,7 @@ def test_wave_kernel_long_and_empty_queries(gpu, T):
     index = _idx(ip, ix, dt, N)
     for k in (1, 30, 200):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
-        sampled = _sample_p(index.info()["n_tiles"], k) > 1
-        assert index.last_dispatch()["kernels"] == (WAVE_SAMPLED if sampled else {"wave_all"})
+        assert index.last_dispatch()["kernels"] == _want_kernels(_geom_p(index, k, T=T), flat=False)
     index.set_option("sample_p", 1)  # the exact pass over every tile
     _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
     assert index.last_dispatch()["kernels"] == {"wave_all"}
@@ -417,6 +427,22 @@ def _sample_p(ntiles, k, W=1, pmax=8):
     return 1
 
 
+def _geom_p(index, k, W=1, ntiles=None, opts=None, T=8):
+    """The threshold geometry search_geom picks (bm25mi_kernels.hip): 0 =
+    tile-bound keys (a sampled geometry, the index keeps tile bounds,
+    theta_bound on, queries of 1..8 terms, at most 30720 tiles, a collection
+    of >= 16k tiles), else _sample_p's stride."""
+    opts = opts or {}
+    info = index.info()
+    nt = info["n_tiles"] if ntiles is None else ntiles
+    pmax = opts.get("sample_p", 8)
+    P = _sample_p(nt, k, W, pmax)
+    if (P > 1 and opts.get("theta_bound", 1) and info["tile_bounds"] and 1 <= T <= 8
+            and nt <= 30720 and nt * W >= 16 * k):
+        return 0
+    return P
+
+
 # (options, segment table)
 VARIANTS = [
     ({}, "dense"), ({"sample_p": 1}, "dense"), ({"sample_p": 2}, "dense"),
@@ -446,7 +472,8 @@ def test_kernel_variants_bit_exact(gpu, opts, segments, T):
     q[4, 2:] = q[4, 1]
     index = _idx(ip, ix, dt, N, segments=segments)
     _exact(index.search(q, 7), oracle.search_c(N, ip, ix, dt, q, 7))  # defaults first
-    assert index.last_dispatch()["kernels"] == FLAT_SAMPLED
+    assert index.last_dispatch()["kernels"] == _want_kernels(_geom_p(index, 7, T=T))
+    assert index.info()["tile_bounds"] == (segments == "dense")
     for name, val in opts.items():
         index.set_option(name, val)
         assert index.get_option(name) == val
@@ -456,13 +483,12 @@ def test_kernel_variants_bit_exact(gpu, opts, segments, T):
     for k in (1, 7, 100):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
         d = index.last_dispatch()
-        P = _sample_p(ntiles, k, 1, opts.get("sample_p", 8))
-        want = (FLAT_SAMPLED if flat else WAVE_SAMPLED) if P > 1 else \
-            {"flat_all" if flat else "wave_all"}
+        P = _geom_p(index, k, 1, ntiles, opts, T=T)
+        want = _want_kernels(P, flat)
         assert d["kernels"] == want and d["sample_p"] == P, (k, d, want, P)
         if flat:
             assert d["term_lanes"] == (8 if T == 8 else 16)
-            phase = "rest" if P > 1 else "all"
+            phase = "rest" if P != 1 else "all"
             if "flat_bw" in opts:
                 assert d["band_tiles"][phase] == min(opts["flat_bw"], 64 // d["term_lanes"])
         fallback += index.search_stats()["fallback_queries"]
@@ -590,11 +616,17 @@ def test_merge_paths_long_lists(gpu):
     N, V = 6_000_000, 300
     ip, ix, dt = _rand_index(rng, N, V, 400_000)
     q = rng.integers(-1, V, size=(24, 8)).astype(np.int32)
-    index = _idx(ip, ix, dt, N)
+    index = _idx(ip, ix, dt, N, options={"theta_bound": 0})
     for k in (10, 250, 600, 1500):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
-        assert index.last_dispatch()["sample_p"] == _sample_p(index.info()["n_tiles"], k)
+        assert index.last_dispatch()["sample_p"] == _geom_p(index, k, opts={"theta_bound": 0})
         assert index.search_stats()["fallback_queries"] == 0
+    # the tile-bound threshold on this index (every term equally weighted, so
+    # a tile's largest single-term score is far below the best sums): lists
+    # overflow and the queries take the exact fallback stage — still exact
+    index.set_option("theta_bound", 1)
+    _exact(index.search(q, 10), oracle.search_c(N, ip, ix, dt, q, 10))
+    assert index.last_dispatch()["sample_p"] == 0
 
 
 def test_rare_queries_zero_fill_path(gpu):
@@ -964,7 +996,7 @@ def test_config4_c3_index_eight_shards_full_batch(gpu):
         _progress(f"c4: rank shard [{lo}, {hi}) built")
     _exact(_protocol_search(shards, torch.from_numpy(q).cuda(), cfg.k, sdm), ref)
     d = shards[0].last_dispatch()
-    assert d["kernels"] == FLAT_SAMPLED, d
+    assert d["kernels"] == _want_kernels(_geom_p(shards[0], cfg.k, W, (sdm + 2047) // 2048)), d
     for s in shards:
         s.close()
 
@@ -989,7 +1021,8 @@ def test_config5_rank_shard_full_batch(gpu, segments):
     _progress(f"c5: {segments} index built")
     assert index.info()["sparse"] == (segments == "sparse")
     _exact(index.search(q, cfg.k), (rd + lo, rs))
-    assert index.last_dispatch()["kernels"] == FLAT_SAMPLED
+    assert index.last_dispatch()["kernels"] == _want_kernels(_geom_p(index, cfg.k))
+    assert index.info()["tile_bounds"] == (segments == "dense")
     assert index.search_stats()["fallback_queries"] == 0
     index.close()
 
@@ -1017,7 +1050,7 @@ def test_rccl_all_gather_branch(gpu):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("T", [4, 12])
+@pytest.mark.parametrize("T", [4, 8])
 def test_tile_bound_skips_exact(gpu, T):
     """The REST pass skips the (query, tile) pairs whose query-term maxima
     (f16 upper bounds per (term, tile)) sum below the threshold: same bits
@@ -1071,15 +1104,15 @@ def _bound_case(seed, N, V, heavy, big=False):
     return np.array(indptr, np.int64), np.concatenate(idx), np.concatenate(dat)
 
 
-@pytest.mark.parametrize("T,big", [(4, False), (12, False), (9, True), (70, False)])
+@pytest.mark.parametrize("T,big", [(4, False), (8, True), (3, True), (12, False), (70, False)])
 def test_theta_bound_exact(gpu, T, big):
     """Threshold keys from the tile bounds (theta_bound, no SAMPLE pass): the
     same bits as the sampled threshold and as the oracle, with and without
     the REST tile skip — ties at the threshold (quarter-step values), rows
-    with fewer positive tiles than k (zero-fill), padding, duplicates, ids
-    >= V, scores past f16's range and below its subnormals, and T > 64 (the
-    wave kernel's REST)."""
-    N, V = 1_500_000, 300
+    with fewer positive tiles than k (zero-fill), padding, duplicates, scores
+    past f16's range and below its subnormals, and T > 64 (the wave kernel's
+    REST)."""
+    N, V = 3_500_000, 300  # 1709 tiles: >= 16k at k = 100 (search_geom)
     ip, ix, dt = _bound_case(70 + T, N, V, 30, big)
     rng = np.random.default_rng(T)
     q = np.concatenate([rng.integers(0, 30, size=(40, T // 2)),
@@ -1088,7 +1121,6 @@ def test_theta_bound_exact(gpu, T, big):
     q[1, 1:] = q[1, 0]
     q[2, :] = -1
     q[2, 0] = 30 + int(np.argmin(np.diff(ip)[30:]))  # one rare term: < k positive tiles
-    q[3, -1] = V + 5
     index = _idx(ip, ix, dt, N, segments="dense")
     assert index.get_option("theta_bound") == 1
     for k in (1, 10, 100):
@@ -1099,8 +1131,9 @@ def test_theta_bound_exact(gpu, T, big):
                 index.set_option("tile_bound", tl)
                 _exact(index.search(q, k), ref)
                 d = index.last_dispatch()
-                assert ("bound_keys" in d["kernels"]) == bool(tb), (tb, d)
-                assert (d["sample_p"] == 0) == bool(tb), d
+                P = _geom_p(index, k, opts={"theta_bound": tb}, T=T)
+                assert (P == 0) == (bool(tb) and T <= 8), (P, tb, T)
+                assert d["kernels"] == _want_kernels(P, flat=T <= 64) and d["sample_p"] == P, d
     index.set_option("theta_bound", 1)
     index.set_option("tile_bound", 1)
     index.close()
@@ -1130,9 +1163,9 @@ def test_theta_bound_sharded_protocol(gpu):
     W = len(shards)
     smax = max(hi - lo for lo, hi in zip(cuts[:-1], cuts[1:]))
     dq = torch.from_numpy(q).cuda()
-    for k in (10, 100):
+    for k in (10, 16):  # (3 x 93 tiles >= 16k)
         S = shards[0].sample_width(k, W, smax)
-        assert S == k, S
+        assert S > 0 and S * W >= 2 * k, S
         keys = torch.zeros((W, q.shape[0], S), dtype=torch.int64, device="cuda")
         for r, s in enumerate(shards):
             s.search_sample_device(dq, k, W, smax, keys[r])
