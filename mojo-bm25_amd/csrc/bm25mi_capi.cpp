@@ -488,9 +488,9 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
   // tile bounds of the REST pass (dense table, non-negative index); without
   // the memory the search simply runs without them
   if (!ix.sparse && ix.nonneg && n_terms > 0 && ntiles > 0) {
-    if (hipMalloc(&ix.bmax, sizeof(uint16_t) * n_terms * ntiles) == hipSuccess) {
+    if (hipMalloc(&ix.bmax, sizeof(uint16_t) * n_terms * bmax_stride(ntiles)) == hipSuccess) {
       TRYC(launch_build_bmax(ix, h->stream), "build_bmax launch");
-      h->device_bytes += (int64_t)(sizeof(uint16_t) * n_terms * ntiles);
+      h->device_bytes += (int64_t)(sizeof(uint16_t) * n_terms * bmax_stride(ntiles));
     } else {
       (void)hipGetLastError();
       ix.bmax = nullptr;
@@ -559,7 +559,7 @@ int bm25_index_bounds(const bm25_index* h, int32_t* has_bounds, int64_t* bytes) 
   if (!h) return fail(BM25_EINVAL, "NULL index");
   const bool on = h->ix.bmax != nullptr;
   if (has_bounds) *has_bounds = on ? 1 : 0;
-  if (bytes) *bytes = on ? (int64_t)sizeof(uint16_t) * h->ix.n_terms * h->ix.ntiles : 0;
+  if (bytes) *bytes = on ? (int64_t)sizeof(uint16_t) * h->ix.n_terms * bmax_stride(h->ix.ntiles) : 0;
   return BM25_OK;
 }
 

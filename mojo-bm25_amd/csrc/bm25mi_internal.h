@@ -91,6 +91,9 @@ struct Dispatch {
   int32_t sample_p = 0;       // sampling stride (1: exact pass, 0: tile-bound keys)
 };
 
+// Row stride of the tile-bound table: whole groups of four tiles (8 B).
+__host__ __device__ inline int64_t bmax_stride(int64_t ntiles) { return (ntiles + 3) & ~(int64_t)3; }
+
 struct DevIndex {
   int device = 0;
   int64_t n_docs = 0, n_terms = 0, nnz = 0, doc_offset = 0;
@@ -113,7 +116,7 @@ struct DevIndex {
   uint16_t* ldoc = nullptr;
   float* val = nullptr;
   // Tile bounds (dense segment table, non-negative index): each (term,
-  // tile)'s largest score as f16 bits rounded DOWN, [V][ntiles] — a lower
+  // tile)'s largest score as f16 bits rounded DOWN, [V][bmax_stride] — a lower
   // bound of that score (threshold keys) and, one f16 step up, an upper bound
   // (the REST pass's tile skip)
   uint16_t* bmax = nullptr;

@@ -991,7 +991,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     d.aux = 0u;
     if (PH == kRest && a.bmax != nullptr) {  // > the term's largest score in the tile: one
       // f16 step above its rounded-down maximum
-      if (ok) d.aux = (uint32_t)a.bmax[tt * a.ntiles + tile] + 1u;
+      if (ok) d.aux = (uint32_t)a.bmax[tt * bmax_stride(a.ntiles) + tile] + 1u;
     } else if (skipping) {  // the score-key half of this tile's best sample key
       // G and P are powers of two (sample_geom): shifts, no integer division
       const uint32_t t32 = (uint32_t)tile;
@@ -1428,7 +1428,8 @@ __global__ __launch_bounds__(256) void build_tables_kernel(
 }
 
 // Tile bounds (dense segment table, non-negative index): bmax[t][j] = term
-// t's largest score in tile j as f16 bits rounded down (0: no posting there;
+// t's largest score in tile j as f16 bits rounded down (rows of
+// bmax_stride(ntiles) entries, zero past the last tile; 0: no posting there;
 // 65504 past f16's range), one block per term (coalesced over its tiles), the
 // segments from the rel table.  The value is <= the real maximum (a lower
 // bound: bound_keys_kernel) and the next f16 up is > it (an upper bound: the
@@ -1438,9 +1439,11 @@ __global__ __launch_bounds__(256) void build_bmax_kernel(const int64_t* __restri
                                                          const float* __restrict__ val, int64_t V,
                                                          int64_t ntiles,
                                                          uint16_t* __restrict__ bmax) {
+  const int64_t bs = bmax_stride(ntiles);
   for (int64_t t = blockIdx.x; t < V; t += gridDim.x) {
     const int64_t ip = indptr[t];
     const uint32_t* r = rel + t * (ntiles + 1);
+    for (int64_t j = ntiles + threadIdx.x; j < bs; j += blockDim.x) bmax[t * bs + j] = 0;
     for (int64_t j = threadIdx.x; j < ntiles; j += blockDim.x) {
       float m = 0.f;
       for (int64_t p = ip + r[j]; p < ip + r[j + 1]; ++p) m = fmaxf(m, val[p]);
@@ -1448,13 +1451,13 @@ __global__ __launch_bounds__(256) void build_bmax_kernel(const int64_t* __restri
       uint16_t u;
       __builtin_memcpy(&u, &h, 2);
       if ((float)h > m) --u;  // (inf past the range becomes 65504)
-      bmax[t * ntiles + j] = u;
+      bmax[t * bs + j] = u;
     }
   }
 }
 
-// Tile-bound threshold keys (search_geom's P = 0), one wave per query: for
-// every tile j, lb_j = the largest of its query terms' tile maxima (bmax,
+// Tile-bound threshold keys (search_geom's P = 0), one workgroup per query:
+// for every tile j, lb_j = the largest of its query terms' tile maxima (bmax,
 // rounded down).  A document of the tile that holds such a maximum scores at
 // least lb_j — its sum includes that term's score, and fp32 additions of
 // non-negative values never decrease — so the key (lb_j, the tile's LAST
@@ -1463,65 +1466,107 @@ __global__ __launch_bounds__(256) void build_bmax_kernel(const int64_t* __restri
 // key, like the SAMPLE pass's keys, with no posting scored.  Writes this
 // shard's best S keys of every query (global doc ids; 0: fewer positive
 // tiles).  LDS: the tiles' lb_j as f16 bits (ordered as integers: all >= 0).
-__global__ __launch_bounds__(64) void bound_keys_kernel(IndexArgs a,
-                                                        const uint16_t* __restrict__ bmax,
-                                                        const int32_t* __restrict__ queries,
-                                                        int32_t T, int32_t S_log2, int64_t S,
-                                                        uint64_t* __restrict__ keys) {
-  extern __shared__ uint16_t lbv[];
+// The four waves read the bmax rows (T <= kBoundMaxTerms = 8 loads per tile
+// in flight, coalesced over consecutive tiles: T * ntiles * 2 B per query);
+// wave 0 then selects and writes from LDS.
+constexpr int kBoundNT = 256;
+__global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
+                                                              const uint16_t* __restrict__ bmax,
+                                                              const int32_t* __restrict__ queries,
+                                                              int32_t T, int32_t S_log2, int64_t S,
+                                                              uint64_t* __restrict__ keys) {
+  extern __shared__ uint64_t lbq[];  // lb_j as u16, four tiles per u64 (zero past the last)
   const int64_t q = blockIdx.x;
-  const uint32_t lane = lane_id();
   const int32_t nt = (int32_t)a.ntiles;
-  // the query's terms as scalar loads (uniform addresses; padding and ids
-  // >= V: none).  Not a readlane of a per-lane copy: the compiler may compute
-  // that copy only in the lanes of the divergent tile loop that uses it.
+  const int32_t nq4 = (nt + 3) >> 2;      // u64 groups of four tiles
+  const int64_t bs = bmax_stride(a.ntiles);  // a row holds whole groups (zero-padded)
+  // the query's terms (T <= 8, launch_sample checks), loaded at uniform
+  // addresses with every lane active; padding and ids >= V: none
   const int32_t* qt = queries + q * T;
-  for (int32_t j = (int32_t)lane; j < nt; j += 64) {  // (a lane's own tiles only)
-    uint32_t m = 0u;
-    for (int32_t i = 0; i < T; ++i) {
-      const int32_t t = __builtin_amdgcn_readfirstlane(qt[i]);
-      if (t >= 0 && (int64_t)t < a.V) m = max(m, (uint32_t)bmax[(int64_t)t * nt + j]);
+  const uint64_t* row[kBoundMaxTerms];
+  bool has[kBoundMaxTerms];
+#pragma unroll
+  for (int i = 0; i < (int)kBoundMaxTerms; ++i) {
+    const int32_t t = i < T ? __builtin_amdgcn_readfirstlane(qt[i]) : -1;
+    has[i] = t >= 0 && (int64_t)t < a.V;
+    row[i] = reinterpret_cast<const uint64_t*>(bmax + (has[i] ? (int64_t)t * bs : 0));
+  }
+  for (int32_t g = (int32_t)threadIdx.x; g < nq4; g += kBoundNT) {
+    uint64_t v[kBoundMaxTerms];
+#pragma unroll
+    for (int i = 0; i < (int)kBoundMaxTerms; ++i) v[i] = has[i] ? row[i][g] : 0ull;
+    uint64_t m = 0ull;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint32_t x = 0u;
+#pragma unroll
+      for (int i = 0; i < (int)kBoundMaxTerms; ++i) x = max(x, (uint32_t)(v[i] >> (16 * u)) & 0xFFFFu);
+      m |= (uint64_t)x << (16 * u);
     }
-    lbv[j] = (uint16_t)m;
+    lbq[g] = m;
   }
   __syncthreads();
+  if (threadIdx.x >= 64) return;  // wave 0 alone from here (no more barriers)
+  const uint32_t lane = lane_id();
   // the k-th largest lb (k = S), bit by bit from the top: a bit of the answer
   // is set iff at least `need` values match its prefix with that bit set
+  // (padding tiles hold 0: they never match a set bit)
   uint32_t v = 0u, need = (uint32_t)S;
   for (int bit = 15; bit >= 0; --bit) {
-    const uint32_t hm = 0xFFFFu << bit, cand = v | (1u << bit);
+    const uint32_t hm = (0xFFFFu << bit) & 0xFFFFu, cand = v | (1u << bit);  // (16-bit values)
     uint32_t c = 0u;
-    for (int32_t j = (int32_t)lane; j < nt; j += 64) c += ((uint32_t)lbv[j] & hm) == cand;
+#pragma unroll 4
+    for (int32_t g = (int32_t)lane; g < nq4; g += 64) {
+      const uint64_t x = lbq[g];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) c += (((uint32_t)(x >> (16 * u)) & hm) == cand);
+    }
     const uint32_t tot = wave_sum_u32(c);
     if (tot >= need) v = cand;
     else need -= tot;
   }
   // fewer than k positive tiles (v = 0): every positive one, zeros after it.
   // Otherwise the tiles above v and the first `need` tiles at v (lowest tile
-  // first: their keys are the larger ones), compacted in tile order.
+  // first: their keys are the larger ones), compacted in tile order (a lane's
+  // four tiles in order, then the lanes in order).
   uint32_t eq_seen = 0u, kept = 0u;
   uint64_t* out = keys + q * S;
-  const int32_t nchunk = (nt + 63) >> 6;
-  for (int32_t c = 0; c < nchunk; ++c) {
-    const int32_t j = c * 64 + (int32_t)lane;
-    const uint32_t x = j < nt ? (uint32_t)lbv[j] : 0u;
-    const bool eq = v != 0u && x == v;
-    const uint64_t em = __ballot(eq);
-    const uint32_t erank = eq_seen + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-    const bool keep = x > v || (eq && erank < need);
-    const uint64_t km = __ballot(keep);
-    const uint32_t pos = kept + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
-                                             __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
-    if (keep && (int64_t)pos < S) {
-      const int64_t last = min(((int64_t)j + 1) << S_log2, a.n_docs) - 1 + a.doc_offset;
-      _Float16 h;
-      const uint16_t xb = (uint16_t)x;
-      __builtin_memcpy(&h, &xb, 2);
-      out[pos] = ((uint64_t)score_key((float)h) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)last);
+  for (int32_t g0 = 0; g0 < nq4; g0 += 64) {
+    const int32_t g = g0 + (int32_t)lane;
+    const uint64_t x = g < nq4 ? lbq[g] : 0ull;
+    uint32_t ne = 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ne += v != 0u && ((uint32_t)(x >> (16 * u)) & 0xFFFFu) == v;
+    const uint32_t ie = wave_incl_scan(ne);
+    uint32_t er = eq_seen + ie - ne;  // ties before this lane's first tile
+    uint32_t keep4 = 0u, nk = 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t xu = (uint32_t)(x >> (16 * u)) & 0xFFFFu;
+      const bool eq = v != 0u && xu == v;
+      const bool keep = xu > v || (eq && er < need);
+      er += eq ? 1u : 0u;
+      keep4 |= keep ? (1u << u) : 0u;
+      nk += keep ? 1u : 0u;
     }
-    eq_seen += (uint32_t)__popcll(em);
-    kept += (uint32_t)__popcll(km);
+    const uint32_t ik = wave_incl_scan(nk);
+    uint32_t pos = kept + ik - nk;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if ((keep4 >> u) & 1u) {
+        if ((int64_t)pos < S) {
+          const int64_t j = 4 * (int64_t)g + u;
+          const int64_t last = min((j + 1) << S_log2, a.n_docs) - 1 + a.doc_offset;
+          _Float16 h;
+          const uint16_t xb = (uint16_t)(x >> (16 * u));
+          __builtin_memcpy(&h, &xb, 2);
+          out[pos] = ((uint64_t)score_key((float)h) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)last);
+        }
+        ++pos;
+      }
+    }
+    eq_seen += (uint32_t)__shfl((int)ie, 63, 64);
+    kept += (uint32_t)__shfl((int)ik, 63, 64);
   }
   for (int64_t p = (int64_t)kept + lane; p < S; p += 64) out[p] = 0ull;
 }
@@ -1935,6 +1980,11 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
 constexpr int kFastR = 32;      // list keys per lane held in registers
 constexpr int kFastMaxK = 1024; // largest k served (LDS: k keys per wave)
 
+__device__ __forceinline__ void wave_sort_write(uint64_t* keys, uint32_t n, int m, int32_t k,
+                                                int64_t doc_offset, int64_t q,
+                                                int32_t* __restrict__ docs,
+                                                float* __restrict__ scores);
+
 // The body of merge_fast_kernel for a list held in R keys per lane.
 template <int R>
 __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64_t doc_offset,
@@ -2004,6 +2054,17 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
                                             __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
     base += (uint32_t)__popcll(b);
   }
+  wave_sort_write(keys, n, m, k, doc_offset, q, docs, scores);
+}
+
+// The n keys in keys[0, n) (the wave's LDS slice, m = next_pow2 >= n) ->
+// sorted best first; the first k written as docs / scores of row q
+// (padding past n: doc -1, score bits ~0).
+__device__ __forceinline__ void wave_sort_write(uint64_t* keys, uint32_t n, int m, int32_t k,
+                                                int64_t doc_offset, int64_t q,
+                                                int32_t* __restrict__ docs,
+                                                float* __restrict__ scores) {
+  const uint32_t lane = lane_id();
   for (int i = (int)n + (int)lane; i < m; i += 64) keys[i] = 0ull;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   for (int size = 2; size <= m; size <<= 1) {
@@ -2033,10 +2094,81 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
   }
 }
 
+// A list longer than the registers hold (64 kFastR < cnt <= C: a query
+// whose threshold sits far below its k-th key), one wave: the k-th largest
+// score half by a radix selection over the list in memory (four 8-bit
+// digits, a wave-private LDS histogram), then the keys above that score and
+// all keys at it compacted into the wave's LDS slice and sorted.  Returns
+// false (nothing written) when score ties make that more than kFastMaxK
+// keys: the block merge takes the query.
+__device__ bool long_merge_one(const Stage& sg, int32_t k, int64_t doc_offset, int64_t q,
+                               int32_t cnt, uint64_t* keys, uint32_t* h,
+                               int32_t* __restrict__ docs, float* __restrict__ scores) {
+  const uint32_t lane = lane_id();
+  const uint64_t* lst = sg.list + q * (int64_t)sg.C;
+  uint32_t prefix = 0u, need = (uint32_t)k;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int b = (int)lane; b < 256; b += 64) h[b] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int hs = shift + 8;
+    for (int i = (int)lane; i < cnt; i += 64) {  // (atomics only: no cross-lane ops)
+      const uint32_t x = (uint32_t)(lst[i] >> 32);
+      if (hs >= 32 || (x >> hs) == (prefix >> hs)) atomicAdd(&h[(x >> shift) & 255u], 1u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    uint32_t c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = h[4 * lane + j];
+    const uint32_t t = c[0] + c[1] + c[2] + c[3];
+    uint32_t incl = t;  // inclusive scan over the lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+      if ((int)lane >= o) incl += y;
+    }
+    const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
+    uint32_t above = tot - incl;  // keys in the bins of the higher lanes
+    uint32_t d1 = 0u, pneed = 0u;  // (digit + 1, rank in its bin) of the one lane holding it
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+      if (above < need && need <= above + c[j]) {
+        d1 = 4u * lane + (uint32_t)j + 1u;
+        pneed = need - above;
+      }
+      above += c[j];
+    }
+    d1 = wave_max_u32(d1);
+    pneed = wave_max_u32(pneed);
+    if (d1 == 0u) return false;  // (cannot happen: need <= the keys of the prefix)
+    prefix |= (d1 - 1u) << shift;
+    need = pneed;
+  }
+  // keys of score > prefix, then every key of score == prefix
+  uint32_t base = 0u;
+  const int rounds = (cnt + 63) >> 6;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int r = 0; r < rounds; ++r) {
+      const int i = r * 64 + (int)lane;
+      const uint64_t x = i < cnt ? lst[i] : 0ull;
+      const uint32_t hi = (uint32_t)(x >> 32);
+      const bool keep = x != 0ull && (pass == 0 ? hi > prefix : hi == prefix);
+      const uint64_t b = __ballot(keep);
+      const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+      if (keep && pos < (uint32_t)kFastMaxK) keys[pos] = x;
+      base += (uint32_t)__popcll(b);
+    }
+  }
+  if (base > (uint32_t)kFastMaxK) return false;
+  wave_sort_write(keys, base, next_pow2(base > 1u ? (int)base : 2), k, doc_offset, q, docs, scores);
+  return true;
+}
+
 __global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, int64_t doc_offset,
                                                          Workspace ws, int32_t* __restrict__ docs,
                                                          float* __restrict__ scores) {
   __shared__ uint64_t sk[4][kFastMaxK];
+  __shared__ uint32_t hist[4][256];
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= sg.nq_host) return;  // wave-uniform; no barriers in this kernel
   const uint32_t lane = lane_id();
@@ -2050,6 +2182,9 @@ __global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, in
     }
     return;
   }
+  if (cnt > 64 * kFastR && long_merge_one(sg, k, doc_offset, q, cnt, keys,
+                                           hist[threadIdx.x >> 6], docs, scores))
+    return;
   if (cnt > 64 * kFastR || (th == kZeroFillTheta && cnt < k)) {
     if (lane == 0) ws.slow[atomicAdd(ws.counters + 4, 1)] = (int32_t)q;
     return;
@@ -2568,12 +2703,12 @@ hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q
     return hipGetLastError();
   }
   if (g.P == 0) {  // tile-bound keys: no posting is scored before REST
-    if (ix.bmax == nullptr || ix.ntiles > kBoundMaxTiles || Q > 0x7FFFFFFF)
+    if (ix.bmax == nullptr || ix.ntiles > kBoundMaxTiles || Q > 0x7FFFFFFF || T > kBoundMaxTerms)
       return hipErrorInvalidValue;
     if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, d_queries, Q, T, ws, stream);
     ix.disp.kernels |= kKBound;
-    hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(64),
-                       (size_t)((ix.ntiles * 2 + 15) & ~15ll), stream, args_of(ix), ix.bmax,
+    hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT),
+                       (size_t)(bmax_stride(ix.ntiles) * 2), stream, args_of(ix), ix.bmax,
                        d_queries, (int32_t)T, ix.tile_shift, g.S, keys);
     return hipGetLastError();
   }
