@@ -1506,39 +1506,54 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
     lbq[g] = m;
   }
   __syncthreads();
-  if (threadIdx.x >= 64) return;  // wave 0 alone from here (no more barriers)
-  const uint32_t lane = lane_id();
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  __shared__ uint32_t wtot[2][kBoundNT / 64];  // per-wave partials (double-buffered)
   // the k-th largest lb (k = S), bit by bit from the top: a bit of the answer
   // is set iff at least `need` values match its prefix with that bit set
-  // (padding tiles hold 0: they never match a set bit)
+  // (padding tiles hold 0: they never match a set bit); every thread counts
+  // its groups, the waves' counts meet in LDS (one barrier per bit)
   uint32_t v = 0u, need = (uint32_t)S;
   for (int bit = 15; bit >= 0; --bit) {
     const uint32_t hm = (0xFFFFu << bit) & 0xFFFFu, cand = v | (1u << bit);  // (16-bit values)
     uint32_t c = 0u;
-#pragma unroll 4
-    for (int32_t g = (int32_t)lane; g < nq4; g += 64) {
+    for (int32_t g = (int32_t)threadIdx.x; g < nq4; g += kBoundNT) {
       const uint64_t x = lbq[g];
 #pragma unroll
       for (int u = 0; u < 4; ++u) c += (((uint32_t)(x >> (16 * u)) & hm) == cand);
     }
-    const uint32_t tot = wave_sum_u32(c);
+    c = wave_sum_u32(c);
+    if (lane == 0) wtot[bit & 1][wv] = c;
+    __syncthreads();
+    uint32_t tot = 0u;
+#pragma unroll
+    for (int w = 0; w < kBoundNT / 64; ++w) tot += wtot[bit & 1][w];
     if (tot >= need) v = cand;
     else need -= tot;
   }
   // fewer than k positive tiles (v = 0): every positive one, zeros after it.
   // Otherwise the tiles above v and the first `need` tiles at v (lowest tile
-  // first: their keys are the larger ones), compacted in tile order (a lane's
-  // four tiles in order, then the lanes in order).
+  // first: their keys are the larger ones), compacted in tile order: rounds
+  // of 256 groups, a thread's four tiles in order, then the threads in order
+  // (a scan inside each wave, the waves' totals through LDS).
+  __shared__ uint32_t wsc[2][kBoundNT / 64];
   uint32_t eq_seen = 0u, kept = 0u;
   uint64_t* out = keys + q * S;
-  for (int32_t g0 = 0; g0 < nq4; g0 += 64) {
-    const int32_t g = g0 + (int32_t)lane;
+  for (int32_t g0 = 0; g0 < nq4; g0 += kBoundNT) {
+    const int32_t g = g0 + (int32_t)threadIdx.x;
     const uint64_t x = g < nq4 ? lbq[g] : 0ull;
     uint32_t ne = 0u;
 #pragma unroll
     for (int u = 0; u < 4; ++u) ne += v != 0u && ((uint32_t)(x >> (16 * u)) & 0xFFFFu) == v;
     const uint32_t ie = wave_incl_scan(ne);
-    uint32_t er = eq_seen + ie - ne;  // ties before this lane's first tile
+    if (lane == 63) wsc[0][wv] = ie;
+    __syncthreads();
+    uint32_t ebase = eq_seen, etot = 0u;
+#pragma unroll
+    for (int w = 0; w < kBoundNT / 64; ++w) {
+      ebase += w < (int)wv ? wsc[0][w] : 0u;
+      etot += wsc[0][w];
+    }
+    uint32_t er = ebase + ie - ne;  // ties before this thread's first tile
     uint32_t keep4 = 0u, nk = 0u;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1550,7 +1565,15 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
       nk += keep ? 1u : 0u;
     }
     const uint32_t ik = wave_incl_scan(nk);
-    uint32_t pos = kept + ik - nk;
+    if (lane == 63) wsc[1][wv] = ik;
+    __syncthreads();
+    uint32_t kbase = kept, ktot = 0u;
+#pragma unroll
+    for (int w = 0; w < kBoundNT / 64; ++w) {
+      kbase += w < (int)wv ? wsc[1][w] : 0u;
+      ktot += wsc[1][w];
+    }
+    uint32_t pos = kbase + ik - nk;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if ((keep4 >> u) & 1u) {
@@ -1565,10 +1588,11 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
         ++pos;
       }
     }
-    eq_seen += (uint32_t)__shfl((int)ie, 63, 64);
-    kept += (uint32_t)__shfl((int)ik, 63, 64);
+    eq_seen += etot;
+    kept += ktot;
+    __syncthreads();  // (wsc is rewritten by the next round)
   }
-  for (int64_t p = (int64_t)kept + lane; p < S; p += 64) out[p] = 0ull;
+  for (int64_t p = (int64_t)kept + threadIdx.x; p < S; p += kBoundNT) out[p] = 0ull;
 }
 
 // Sparse segment table, pass 1: ldoc + validation (as build_tables_kernel)
@@ -2111,9 +2135,31 @@ __device__ bool long_merge_one(const Stage& sg, int32_t k, int64_t doc_offset, i
     for (int b = (int)lane; b < 256; b += 64) h[b] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const int hs = shift + 8;
-    for (int i = (int)lane; i < cnt; i += 64) {  // (atomics only: no cross-lane ops)
-      const uint32_t x = (uint32_t)(lst[i] >> 32);
-      if (hs >= 32 || (x >> hs) == (prefix >> hs)) atomicAdd(&h[(x >> shift) & 255u], 1u);
+    // 8 loads in flight per lane; the lanes that share the first pending
+    // lane's digit (most of them: one exponent range) add once
+    for (int i0 = 0; i0 < cnt; i0 += 8 * 64) {
+      uint32_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 64 + (int)lane;
+        x[u] = i < cnt ? (uint32_t)(lst[i] >> 32) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 64 + (int)lane;
+        bool pend = i < cnt && (hs >= 32 || (x[u] >> hs) == (prefix >> hs));
+        const uint32_t dig = (x[u] >> shift) & 255u;
+        const uint64_t m = __ballot(pend);
+        if (m != 0ull) {  // wave-uniform
+          const int leader = __builtin_ctzll(m);
+          const uint32_t dl = (uint32_t)__shfl((int)dig, leader, 64);
+          const bool same = pend && dig == dl;
+          const uint64_t sm = __ballot(same);
+          if ((int)lane == leader) atomicAdd(&h[dl], (uint32_t)__popcll(sm));
+          pend = pend && !same;
+        }
+        if (pend) atomicAdd(&h[dig], 1u);
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     uint32_t c[4];
@@ -2143,19 +2189,22 @@ __device__ bool long_merge_one(const Stage& sg, int32_t k, int64_t doc_offset, i
     prefix |= (d1 - 1u) << shift;
     need = pneed;
   }
-  // keys of score > prefix, then every key of score == prefix
+  // every key of score >= the k-th key's score (the sort below orders them)
   uint32_t base = 0u;
-  const int rounds = (cnt + 63) >> 6;
-  for (int pass = 0; pass < 2; ++pass) {
-    for (int r = 0; r < rounds; ++r) {
-      const int i = r * 64 + (int)lane;
-      const uint64_t x = i < cnt ? lst[i] : 0ull;
-      const uint32_t hi = (uint32_t)(x >> 32);
-      const bool keep = x != 0ull && (pass == 0 ? hi > prefix : hi == prefix);
+  for (int i0 = 0; i0 < cnt; i0 += 8 * 64) {
+    uint64_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + (int)lane;
+      x[u] = i < cnt ? lst[i] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool keep = x[u] != 0ull && (uint32_t)(x[u] >> 32) >= prefix;
       const uint64_t b = __ballot(keep);
       const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-      if (keep && pos < (uint32_t)kFastMaxK) keys[pos] = x;
+      if (keep && pos < (uint32_t)kFastMaxK) keys[pos] = x[u];
       base += (uint32_t)__popcll(b);
     }
   }
