@@ -1474,7 +1474,10 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
                                                               const uint16_t* __restrict__ bmax,
                                                               const int32_t* __restrict__ queries,
                                                               int32_t T, int32_t S_log2, int64_t S,
-                                                              uint64_t* __restrict__ keys) {
+                                                              uint64_t* __restrict__ keys,
+                                                              uint64_t* __restrict__ theta,
+                                                              int32_t* __restrict__ list_cnt,
+                                                              int32_t* __restrict__ counters) {
   extern __shared__ uint64_t lbq[];  // lb_j as u16, four tiles per u64 (zero past the last)
   const int64_t q = blockIdx.x;
   const int32_t nt = (int32_t)a.ntiles;
@@ -1508,6 +1511,76 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
   __syncthreads();
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   __shared__ uint32_t wtot[2][kBoundNT / 64];  // per-wave partials (double-buffered)
+  if (theta != nullptr) {
+    // a single-index search (theta != null, S = k): theta itself — the k-th
+    // key in this index's own doc frame — and the resets theta_wave_kernel
+    // would do (list count, search counters); no key list
+    if (blockIdx.x == 0 && threadIdx.x < kCounters) counters[threadIdx.x] = 0;
+    uint32_t vk = 0u, needk = (uint32_t)S;
+    for (int bit = 15; bit >= 0; --bit) {
+      const uint32_t hm = (0xFFFFu << bit) & 0xFFFFu, cand = vk | (1u << bit);
+      uint32_t c = 0u;
+      for (int32_t g = (int32_t)threadIdx.x; g < nq4; g += kBoundNT) {
+        const uint64_t x = lbq[g];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c += (((uint32_t)(x >> (16 * u)) & hm) == cand);
+      }
+      c = wave_sum_u32(c);
+      if (lane == 0) wtot[bit & 1][wv] = c;
+      __syncthreads();
+      uint32_t tot = 0u;
+#pragma unroll
+      for (int w = 0; w < kBoundNT / 64; ++w) tot += wtot[bit & 1][w];
+      if (tot >= needk) vk = cand;
+      else needk -= tot;
+    }
+    if (vk == 0u) {  // fewer than k positive tiles: every positive doc + zero fill
+      if (threadIdx.x == 0) {
+        theta[q] = (uint64_t)0x80800000u << 32;  // kZeroFillTheta
+        list_cnt[q] = 0;
+      }
+      return;
+    }
+    // the needk-th tile at vk in tile order holds the k-th key
+    __shared__ uint32_t wsk[kBoundNT / 64];
+    uint32_t seen = 0u;
+    for (int32_t g0 = 0; g0 < nq4; g0 += kBoundNT) {
+      const int32_t g = g0 + (int32_t)threadIdx.x;
+      const uint64_t x = g < nq4 ? lbq[g] : 0ull;
+      uint32_t ne = 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ne += ((uint32_t)(x >> (16 * u)) & 0xFFFFu) == vk;
+      const uint32_t ie = wave_incl_scan(ne);
+      if (lane == 63) wsk[wv] = ie;
+      __syncthreads();
+      uint32_t base = seen, tot = 0u;
+#pragma unroll
+      for (int w = 0; w < kBoundNT / 64; ++w) {
+        base += w < (int)wv ? wsk[w] : 0u;
+        tot += wsk[w];
+      }
+      uint32_t r = base + ie - ne;  // ties before this thread's first tile
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (((uint32_t)(x >> (16 * u)) & 0xFFFFu) == vk) {
+          if (r + 1u == needk) {
+            const int64_t j = 4 * (int64_t)g + u;
+            const int64_t last = min((j + 1) << S_log2, a.n_docs) - 1;  // (own doc frame)
+            _Float16 h;
+            const uint16_t xb = (uint16_t)vk;
+            __builtin_memcpy(&h, &xb, 2);
+            theta[q] = ((uint64_t)score_key((float)h) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)last);
+            list_cnt[q] = 0;
+          }
+          ++r;
+        }
+      }
+      seen += tot;
+      if (seen >= needk) return;  // (uniform: every thread saw the same totals)
+      __syncthreads();  // (wsk is rewritten by the next round)
+    }
+    return;
+  }
   // the k-th largest lb (k = S), bit by bit from the top: a bit of the answer
   // is set iff at least `need` values match its prefix with that bit set
   // (padding tiles hold 0: they never match a set bit); every thread counts
@@ -2355,11 +2428,24 @@ __global__ __launch_bounds__(256) void merge_sorted_kernel(
   uint64_t* kb = buf[wave];
   const uint32_t lane = lane_id();
   const int n = W * k;
-  for (int i = (int)lane; i < n; i += 64) {
+  // staged with every load of the wave in flight (n <= 1024: 16 per lane)
+  constexpr int U = kMergeSortedCap / 64;
+  float sv[U];
+  int32_t dv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = u * 64 + (int)lane;
     const int w = i / k, j = i - w * k;
     const int64_t o = (int64_t)w * rstride + q * k + j;
-    kb[i] = make_key(in_scores[o], (uint32_t)in_docs[o]);
+    sv[u] = i < n ? in_scores[o] : 0.f;
+    dv[u] = i < n ? in_docs[o] : 0;
   }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = u * 64 + (int)lane;
+    if (i < n) kb[i] = make_key(sv[u], (uint32_t)dv[u]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   int pos = 0;
   uint64_t head = ((int)lane < W) ? kb[lane * k] : 0ull;
   for (int j = 0; j < k; ++j) {
@@ -2715,7 +2801,7 @@ static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
 template <int S_>
 static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
                      const SampleGeom& g, int W, const uint64_t* all_keys, const Workspace& ws,
-                     hipStream_t st) {
+                     hipStream_t st, bool theta_ready = false) {
   Stage sg = main_stage(ix, Q, g.P, ws);
   if (g.P == 1) {  // no sample pass ran: nothing was zeroed, no segment table built
     hipMemsetAsync(ws.counters, 0, kCounters * sizeof(int32_t), st);
@@ -2731,9 +2817,10 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
     sg.sample_keys = ws.cand;
     sg.sample_stride = g.S;
   }
-  hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, st, all_keys,
-                     (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt, ws.list_cap,
-                     ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs, ws.counters);
+  if (!theta_ready)
+    hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, st,
+                       all_keys, (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt,
+                       ws.list_cap, ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs, ws.counters);
   launch_phase<S_, kRest>(ix, q, T, Q, sg, ws, st);
 }
 
@@ -2758,7 +2845,8 @@ hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q
     ix.disp.kernels |= kKBound;
     hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT),
                        (size_t)(bmax_stride(ix.ntiles) * 2), stream, args_of(ix), ix.bmax,
-                       d_queries, (int32_t)T, ix.tile_shift, g.S, keys);
+                       d_queries, (int32_t)T, ix.tile_shift, g.S, keys, (uint64_t*)nullptr,
+                       (int32_t*)nullptr, (int32_t*)nullptr);
     return hipGetLastError();
   }
 #define CALL(s) sample_s<s>(ix, d_queries, Q, T, g, keys, ws, stream)
@@ -2780,6 +2868,22 @@ hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                         int k, const Workspace& ws, hipStream_t stream) {
   const SampleGeom g = search_geom(ix, ix.ntiles, k, 1, T);
+  if (g.P == 0 && Q > 0 && ix.ntiles > 0) {
+    // one index: the bound kernel selects theta itself (no key list, no theta
+    // kernel)
+    if (ix.bmax == nullptr || ix.ntiles > kBoundMaxTiles || Q > 0x7FFFFFFF || T > kBoundMaxTerms)
+      return hipErrorInvalidValue;
+    if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, d_queries, Q, T, ws, stream);
+    ix.disp.kernels |= kKBound;
+    hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT),
+                       (size_t)(bmax_stride(ix.ntiles) * 2), stream, args_of(ix), ix.bmax,
+                       d_queries, (int32_t)T, ix.tile_shift, (int64_t)k, (uint64_t*)nullptr,
+                       ws.theta, ws.list_cnt, ws.counters);
+#define CALL(s) finish_s<s>(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream, true)
+    BM25_SHIFT_DISPATCH(CALL)
+#undef CALL
+    return hipGetLastError();
+  }
   hipError_t e = launch_sample(ix, d_queries, Q, T, g, ws.cand, ws, stream);
   if (e != hipSuccess) return e;
   return launch_finish(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream);

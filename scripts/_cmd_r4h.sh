@@ -1,8 +1,8 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 P=mojo-bm25_amd/bm25mi/libbm25mi.so
-NAME=r4i STEPS="tests variants" VLIBS="$P" VCFGS="c3 c5" bash scripts/gpu_r4.sh || exit 1
-OUT=$R/gpurun_out/r4i
+NAME=r4j STEPS="tests variants" VLIBS="$P" VCFGS="c3 c5" bash scripts/gpu_r4.sh || exit 1
+OUT=$R/gpurun_out/r4j
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c3_trace -o run -- python3 $R/bench.py --cpu-queries 0 --e2e-batches 0 > $OUT/bench_under_rocprof.json 2> $OUT/bench_rocprof.err || { echo bench trace failed; tail -5 $OUT/bench_rocprof.err; exit 1; }
 python3 -c "

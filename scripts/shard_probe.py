@@ -17,7 +17,7 @@ with RCCL's direct all-gather over the point-to-point xGMI mesh: each rank's
 block goes to its W - 1 peers over W - 1 distinct links in parallel.  The
 constants are stated in the output line.
 
-  python scripts/shard_probe.py [W ...]
+  python scripts/shard_probe.py [W ...]     (env VLIB: a variant library)
 """
 import json
 import os
@@ -28,6 +28,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "mojo-bm25_amd"), REPO]
 import torch  # noqa: E402
 
+if os.environ.get("VLIB"):  # a variant build of libbm25mi (dev: scripts/build_variant.sh)
+    import importlib
+    importlib.import_module("bm25mi.build").LIB = os.path.abspath(os.environ["VLIB"])
 from bm25mi import synth  # noqa: E402
 from bm25mi.index import GpuIndex, merge_sorted_device  # noqa: E402
 
