@@ -380,6 +380,8 @@ def main():
                                    f"{traffic.get('l2_hit_rate')}") if traffic else None,
                 "kernel": ("large-k search (scores_batch_kernel dense sums + lk_* radix "
                            "selection + hipCUB segmented sort)" if large_k else
+                           "score pass (bound_keys_kernel tile-bound threshold + "
+                           "score_flat_kernel REST)" if "bound_keys" in dispatch["kernels"] else
                            "score pass (score_flat_kernel SAMPLE + theta_wave_kernel + "
                            "score_flat_kernel REST)"),
                 "kernel_ms": round(kern_ms, 4),

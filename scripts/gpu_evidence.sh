@@ -29,7 +29,7 @@ i=0
 while read -r tag args ctrs; do
   [ -z "$ctrs" ] && continue
   i=$((i+1))
-  timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-include-regex "score_flat" --output-format csv -d $OUT/pmc_${tag}_p$i -o pmc -- python3 $R/scripts/pmc_workload.py ${args//,/ } > $OUT/pmc_${tag}_p$i.log 2>&1 || { echo pmc pass $i failed; tail -5 $OUT/pmc_${tag}_p$i.log; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-include-regex "score_flat|bound_keys" --output-format csv -d $OUT/pmc_${tag}_p$i -o pmc -- python3 $R/scripts/pmc_workload.py ${args//,/ } > $OUT/pmc_${tag}_p$i.log 2>&1 || { echo pmc pass $i failed; tail -5 $OUT/pmc_${tag}_p$i.log; exit 1; }
 done <<'CTRS'
 c3 --config,c3 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum
 c3 --config,c3 WRITE_SIZE

@@ -3,7 +3,9 @@
 # own time limit and the chain stops at the first failure.
 #   STEPS=tests   pytest -m gpu + smoke
 #   STEPS=lines   bench lines: c3 (CPU legs), c2 (CPU legs), replica proxy
-#                 (rank 0 of 8), c3 at k=10000 (large-k path)
+#                 (rank 0 of 8), c3 at k=10000 (large-k path), c3 at 16
+#                 terms, c5 (one rank's shard)
+#   STEPS=probe   scripts/shard_probe.py (W = PROBE_WS)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 NAME=${NAME:-r4}
@@ -23,6 +25,8 @@ for step in ${STEPS:-tests lines}; do
     timeout -k 10 300 python -u bench.py --config c2 > $OUT/bench_c2.json 2> $OUT/bench_c2.err || { echo bench c2 failed; tail -20 $OUT/bench_c2.err; exit 1; }
     timeout -k 10 300 python -u bench.py --replica-of 8 --cpu-queries 0 > $OUT/bench_replica8.json 2> $OUT/bench_replica8.err || { echo bench replica failed; tail -20 $OUT/bench_replica8.err; exit 1; }
     timeout -k 10 300 python -u bench.py --k 10000 --steps 5 --warmup 2 --cpu-queries 0 --e2e-batches 0 > $OUT/bench_k10000.json 2> $OUT/bench_k10000.err || { echo bench k10000 failed; tail -20 $OUT/bench_k10000.err; exit 1; }
+    timeout -k 10 300 python -u bench.py --terms 16 --cpu-queries 0 > $OUT/bench_t16.json 2> $OUT/bench_t16.err || { echo bench t16 failed; tail -20 $OUT/bench_t16.err; exit 1; }
+    timeout -k 10 600 python -u bench.py --config c5 --cpu-queries 0 --e2e-batches 5 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { echo bench c5 failed; tail -20 $OUT/bench_c5.err; exit 1; }
     ;;
   variants)  # VLIBS: variant libraries timed against the product (scripts/variant_lib_time.py)
     for cfg in ${VCFGS:-c3}; do

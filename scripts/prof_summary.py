@@ -71,7 +71,7 @@ if traffic_out:
                         "write_size_bytes": int(wr), "tcc_ea0_rdreq": int(rd),
                         "l2_hit_rate": round(hit / max(hit + miss, 1), 3),
                         "phases": sorted(ph)})
-    json.dump({"source": os.path.relpath(d), "kernels": "score_flat_kernel ALL + SAMPLE + REST (one search)",
+    json.dump({"source": os.path.relpath(d), "kernels": "the score pass of one search: bound_keys_kernel or score_flat_kernel SAMPLE, score_flat_kernel REST (+ the fallback ALL launch)",
                "method": ("rocprofv3 --pmc, one counter group per pass (scripts/gpu_evidence.sh PART=prof); "
                           "read bytes = TCC_EA0_RDREQ x 128 B, the bytes per request measured for this "
                           "kernel's 4-B and 8-B-per-lane buffer loads by the calibration kernel "
