@@ -180,8 +180,12 @@ SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W, int64_t
 constexpr int64_t kBoundMaxTiles = 30720;
 // ... and at least this many tiles per wanted key over the whole collection.
 constexpr int64_t kBoundTilesPerK = 16;
-// ... and queries of at most this many terms (search_geom).
-constexpr int64_t kBoundMaxTerms = 8;
+// ... and queries of at most this many terms (search_geom; the bound kernel's
+// per-tile loads in flight).
+#ifndef BM25_BOUND_TERMS
+#define BM25_BOUND_TERMS 16
+#endif
+constexpr int64_t kBoundMaxTerms = BM25_BOUND_TERMS;
 
 // Kernel launchers (bm25mi_kernels.hip).  All enqueue on `stream`.
 hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,

@@ -1466,7 +1466,7 @@ __global__ __launch_bounds__(256) void build_bmax_kernel(const int64_t* __restri
 // key, like the SAMPLE pass's keys, with no posting scored.  Writes this
 // shard's best S keys of every query (global doc ids; 0: fewer positive
 // tiles).  LDS: the tiles' lb_j as f16 bits (ordered as integers: all >= 0).
-// The four waves read the bmax rows (T <= kBoundMaxTerms = 8 loads per tile
+// The four waves read the bmax rows (T <= kBoundMaxTerms = 16 loads per tile
 // in flight, coalesced over consecutive tiles: T * ntiles * 2 B per query);
 // wave 0 then selects and writes from LDS.
 constexpr int kBoundNT = 256;
@@ -1483,7 +1483,7 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
   const int32_t nt = (int32_t)a.ntiles;
   const int32_t nq4 = (nt + 3) >> 2;      // u64 groups of four tiles
   const int64_t bs = bmax_stride(a.ntiles);  // a row holds whole groups (zero-padded)
-  // the query's terms (T <= 8, launch_sample checks), loaded at uniform
+  // the query's terms (T <= kBoundMaxTerms, launch_sample checks), loaded at uniform
   // addresses with every lane active; padding and ids >= V: none
   const int32_t* qt = queries + q * T;
   const uint64_t* row[kBoundMaxTerms];
@@ -2542,8 +2542,8 @@ SampleGeom sample_geom(int64_t ntiles, int k, int W, int pmax) {
 // tight threshold while k is a small share of the tiles (at k ~ tiles / 2
 // every query's list overflows) — and queries of at most kBoundMaxTerms
 // terms: a longer query's sum of many terms lies further above its largest
-// single-term score, and its SAMPLE pass pays for itself (measured: 16-term
-// queries at config 3 take 5.34 ms sampled, 5.62 with tile-bound keys).
+// single-term score (16-term queries at config 3: 5.00 ms with tile-bound
+// keys, 5.31 sampled).
 // Otherwise the SAMPLE pass (sample_geom), whose sample tiles report up to
 // 4 real sums each; sample_p = 1 keeps asking for the exact pass.  The key
 // width S is the sampled geometry's either way (so bm25_sample_width needs no
@@ -2612,7 +2612,10 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
   // in groups of 8 tiles: ws.cand holds this shard's sample keys)
   const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kSampleGroup;
   IndexArgs a = args_of(ix);
-  if (skip) a.bmax = nullptr;  // one descriptor field: the sample keys' skip or the tile bounds
+  // one descriptor field: the sample keys' skip or the tile bounds; and the
+  // bounds only at 8 term lanes (16 lanes: 4-tile items whose 16 bmax rows cost
+  // more than the few tiles they skip — 5.45 vs 5.00 ms, 16-term queries)
+  if (skip || TL > 3) a.bmax = nullptr;
   a.seg = ws.seg;
   a.seg_zero = Qb * ((ix.ntiles + 7) >> 3) * 8 * (1 << TL);
   const int64_t nt = PH == kSample ? sample_count(ix.ntiles, sg.P, sg.G) : ix.ntiles;

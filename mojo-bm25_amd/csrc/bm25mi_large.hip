@@ -180,15 +180,26 @@ __global__ __launch_bounds__(64) void lk_pick_kernel(SelState* __restrict__ st,
 }
 
 // The keys >= the k-th key of each query (exactly k: keys are unique),
-// appended in any order (one atomic per wave and round).
+// appended in any order.  A workgroup stages its keys in LDS (an LDS atomic
+// per wave and round) and claims its range of the row with ONE global atomic
+// at the end: the keys are sparse (k of ~N per row, ~k / gridDim.x per
+// workgroup), and a global atomic per wave-round on the row's one counter
+// serialised the pass (8.6 ms per 100-query chunk at k = 10 000).  Keys past
+// the stage's capacity (a zero-fill row's keys crowd into its first docs) take
+// the global atomic directly.
+constexpr int kCompactStage = 2048;
 __global__ __launch_bounds__(256) void lk_compact_kernel(const float* __restrict__ scores,
                                                          int64_t stride, int64_t n_docs,
                                                          const SelState* __restrict__ st,
                                                          int32_t* __restrict__ cnt,
                                                          uint64_t* __restrict__ keys, int64_t kk) {
+  __shared__ uint64_t stage[kCompactStage];
+  __shared__ int32_t n_stage, base;
   const int64_t g = blockIdx.y;
   const uint64_t kth = st[g].prefix;
   const uint32_t lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) n_stage = 0;
+  __syncthreads();
   const float4* row = reinterpret_cast<const float4*>(scores + g * stride);
   const int64_t n4 = (n_docs + 3) >> 2;
   // every lane of a wave runs the same rounds (ballots below)
@@ -211,14 +222,27 @@ __global__ __launch_bounds__(256) void lk_compact_kernel(const float* __restrict
       const bool keep = key != 0ull && key >= kth;
       const uint64_t m = __ballot(keep);
       if (m == 0ull) continue;
-      int base = 0;
-      if (lane == 0) base = atomicAdd(cnt + g, (int)__popcll(m));
-      base = __shfl(base, 0, 64);
-      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (keep && pos < kk) keys[g * kk + pos] = key;
+      int p0 = 0;
+      if (lane == 0) p0 = atomicAdd(&n_stage, (int)__popcll(m));
+      p0 = __shfl(p0, 0, 64);
+      const int pos = p0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (keep) {
+        if (pos < kCompactStage) {
+          stage[pos] = key;
+        } else {  // stage full: straight to the row
+          const int gp = atomicAdd(cnt + g, 1);
+          if (gp < kk) keys[g * kk + gp] = key;
+        }
+      }
     }
   }
+  __syncthreads();
+  const int ns = min(n_stage, kCompactStage);
+  if (threadIdx.x == 0) base = ns > 0 ? atomicAdd(cnt + g, ns) : 0;
+  __syncthreads();
+  for (int j = threadIdx.x; j < ns; j += 256)
+    if (base + j < kk) keys[g * kk + base + j] = stage[j];
 }
 
 // Keys of W best-first lists -> keys[q][w * k + j] (padding maps to key 0).

@@ -17,7 +17,8 @@ with RCCL's direct all-gather over the point-to-point xGMI mesh: each rank's
 block goes to its W - 1 peers over W - 1 distinct links in parallel.  The
 constants are stated in the output line.
 
-  python scripts/shard_probe.py [W ...]     (env VLIB: a variant library)
+  python scripts/shard_probe.py [W ...]     (env VLIB: a variant library;
+                                             PROBE_Q: batch size; PROBE_RANKS, PROBE_ITERS)
 """
 import json
 import os
@@ -47,7 +48,8 @@ def model_gather_us(bytes_per_rank: int, W: int) -> float:
 
 def main():
     cfg = synth.CONFIGS["c3"]
-    q = torch.from_numpy(synth.make_queries(cfg)).cuda()
+    nq = int(os.environ.get("PROBE_Q", "0")) or None  # batch size (default: the config's 1024)
+    q = torch.from_numpy(synth.make_queries(cfg, n_queries=nq)).cuda()
     Q, k = q.shape[0], cfg.k
     dev = q.device.index
     st = torch.cuda.current_stream()

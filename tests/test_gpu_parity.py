@@ -430,14 +430,14 @@ def _sample_p(ntiles, k, W=1, pmax=8):
 def _geom_p(index, k, W=1, ntiles=None, opts=None, T=8):
     """The threshold geometry search_geom picks (bm25mi_kernels.hip): 0 =
     tile-bound keys (a sampled geometry, the index keeps tile bounds,
-    theta_bound on, queries of 1..8 terms, at most 30720 tiles, a collection
+    theta_bound on, queries of 1..16 terms, at most 30720 tiles, a collection
     of >= 16k tiles), else _sample_p's stride."""
     opts = opts or {}
     info = index.info()
     nt = info["n_tiles"] if ntiles is None else ntiles
     pmax = opts.get("sample_p", 8)
     P = _sample_p(nt, k, W, pmax)
-    if (P > 1 and opts.get("theta_bound", 1) and info["tile_bounds"] and 1 <= T <= 8
+    if (P > 1 and opts.get("theta_bound", 1) and info["tile_bounds"] and 1 <= T <= 16
             and nt <= 30720 and nt * W >= 16 * k):
         return 0
     return P
@@ -1132,7 +1132,7 @@ def test_theta_bound_exact(gpu, T, big):
                 _exact(index.search(q, k), ref)
                 d = index.last_dispatch()
                 P = _geom_p(index, k, opts={"theta_bound": tb}, T=T)
-                assert (P == 0) == (bool(tb) and T <= 8), (P, tb, T)
+                assert (P == 0) == (bool(tb) and T <= 16), (P, tb, T)
                 assert d["kernels"] == _want_kernels(P, flat=T <= 64) and d["sample_p"] == P, d
     index.set_option("theta_bound", 1)
     index.set_option("tile_bound", 1)
