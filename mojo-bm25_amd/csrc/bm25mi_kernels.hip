@@ -763,6 +763,10 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
 //     SAMPLE: the tile's best key per slice; ALL: the tile's exact top-4).
 // Each doc's adds stay in query-term order (bm25_native.py:152).
 // ===========================================================================
+// wavefronts per workgroup of the one-wave-per-query kernels (theta_wave,
+// merge_fast, merge_sorted); measured: one-wave workgroups change nothing
+// (profiles/r04/rejected/qw1_*)
+constexpr int kQW = 4;
 #ifndef BM25_FR    // rows in flight (ring slots): REST / ALL, SAMPLE
 #define BM25_FR 10
 #endif
@@ -1882,7 +1886,7 @@ constexpr uint64_t kZeroFillTheta = (uint64_t)0x80800000u << 32;
 // 1024 of them, re-read (L1) otherwise.
 constexpr int kThetaR = 16;  // keys per lane held in registers
 
-__global__ __launch_bounds__(256) void theta_wave_kernel(const uint64_t* __restrict__ all_keys,
+__global__ __launch_bounds__(64 * kQW) void theta_wave_kernel(const uint64_t* __restrict__ all_keys,
                                                          int64_t W, int64_t Q, int64_t S,
                                                          int32_t k, uint64_t* __restrict__ theta,
                                                          int32_t* __restrict__ list_cnt,
@@ -1894,7 +1898,7 @@ __global__ __launch_bounds__(256) void theta_wave_kernel(const uint64_t* __restr
   // counts and the rescore / fallback / block-merge counters (the flat
   // kernel's claim counters reset themselves)
   if (blockIdx.x == 0 && threadIdx.x < kCounters) counters[threadIdx.x] = 0;
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t q = (int64_t)blockIdx.x * kQW + (threadIdx.x >> 6);
   if (q >= Q) return;  // wave-uniform; no barriers
   const uint32_t lane = lane_id();
   const int64_t n = W * S;
@@ -2082,6 +2086,9 @@ __device__ __forceinline__ void wave_sort_write(uint64_t* keys, uint32_t n, int 
                                                 int32_t* __restrict__ docs,
                                                 float* __restrict__ scores);
 
+template <int R>
+__device__ __forceinline__ uint64_t wave_kth_key(const uint64_t (&key)[R], int32_t k, uint32_t& n);
+
 // The body of merge_fast_kernel for a list held in R keys per lane.
 template <int R>
 __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64_t doc_offset,
@@ -2097,9 +2104,31 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
     const uint64_t x = i < cnt ? lst[i] : 0ull;
     key[j] = x >= th ? x : 0ull;  // (every list key is >= theta; key 0 = empty)
   }
-  // kth = the k-th largest key (0: fewer than k keys, all of them are kept)
-  uint64_t kth = 0ull;
   uint32_t n = 0;
+  const uint64_t kth = wave_kth_key<R>(key, k, n);
+  // the n kept keys (>= kth; unique: doc ids differ) -> LDS, sorted best first
+  const int m = next_pow2(n > 1u ? n : 2u);
+  uint32_t base = 0u;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const bool keep = key[j] != 0ull && key[j] >= kth;
+    const uint64_t b = __ballot(keep);
+    if (keep)
+      keys[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
+    base += (uint32_t)__popcll(b);
+  }
+  wave_sort_write(keys, n, m, k, doc_offset, q, docs, scores);
+}
+
+// The k-th largest of a wave's keys held R per lane (key 0 = empty; keys
+// unique otherwise) by a radix selection: the score half bit by bit, then the
+// doc half only among the keys of that score.  Returns 0 when there are at
+// most k keys (all of them are kept); n = the keys kept (min(count, k)).
+template <int R>
+__device__ __forceinline__ uint64_t wave_kth_key(const uint64_t (&key)[R], int32_t k, uint32_t& n) {
+  uint64_t kth = 0ull;
+  n = 0;
 #pragma unroll
   for (int j = 0; j < R; ++j) n += key[j] != 0ull;
   n = wave_sum_u32(n);
@@ -2139,19 +2168,7 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
     kth = ((uint64_t)hi << 32) | lo;
     n = (uint32_t)k;
   }
-  // the n kept keys (>= kth; unique: doc ids differ) -> LDS, sorted best first
-  const int m = next_pow2(n > 1u ? n : 2u);
-  uint32_t base = 0u;
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const bool keep = key[j] != 0ull && key[j] >= kth;
-    const uint64_t b = __ballot(keep);
-    if (keep)
-      keys[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
-    base += (uint32_t)__popcll(b);
-  }
-  wave_sort_write(keys, n, m, k, doc_offset, q, docs, scores);
+  return kth;
 }
 
 // The n keys in keys[0, n) (the wave's LDS slice, m = next_pow2 >= n) ->
@@ -2286,12 +2303,12 @@ __device__ bool long_merge_one(const Stage& sg, int32_t k, int64_t doc_offset, i
   return true;
 }
 
-__global__ __launch_bounds__(256) void merge_fast_kernel(Stage sg, int32_t k, int64_t doc_offset,
+__global__ __launch_bounds__(64 * kQW) void merge_fast_kernel(Stage sg, int32_t k, int64_t doc_offset,
                                                          Workspace ws, int32_t* __restrict__ docs,
                                                          float* __restrict__ scores) {
-  __shared__ uint64_t sk[4][kFastMaxK];
-  __shared__ uint32_t hist[4][256];
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ uint64_t sk[kQW][kFastMaxK];
+  __shared__ uint32_t hist[kQW][256];
+  const int64_t q = (int64_t)blockIdx.x * kQW + (threadIdx.x >> 6);
   if (q >= sg.nq_host) return;  // wave-uniform; no barriers in this kernel
   const uint32_t lane = lane_id();
   uint64_t* keys = sk[threadIdx.x >> 6];
@@ -2409,26 +2426,26 @@ __global__ __launch_bounds__(kMergeNT) void merge_lists_kernel(
   write_result(keys, k, q, 0, docs, scores);
 }
 
-// Merge of W lists that are each sorted best first (bm25_search_finish_
-// device's [Q, k] lists, padding last): one wave per query, the W list heads
-// in lanes 0..W-1; each of the k steps takes the best head (wave max of the
-// u64 key, as two u32 maxima) and advances that list.  A query's lists are
-// staged in LDS first (W * k <= kMergeSortedCap keys); larger merges take
-// merge_lists_kernel.  Keys are unique (global doc ids) except padding (0).
+// Merge of W per-rank [Q, k] lists (bm25_search_finish_device's, padding
+// last): one wave per query holds the W * k keys in registers (16 per lane,
+// all loads in flight), selects the k-th largest key (wave_kth_key) and
+// sorts the k keys at or above it in its LDS slice — a handful of reduction
+// steps instead of k dependent head-advance steps (33 us at W = 8, k = 100).
+// W * k <= kMergeSortedCap; larger merges take merge_lists_kernel.  Keys are
+// unique (global doc ids) except padding (0).
 constexpr int kMergeSortedCap = 1024;  // keys per wave
 
-__global__ __launch_bounds__(256) void merge_sorted_kernel(
+__global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
     const int32_t* __restrict__ in_docs, const float* __restrict__ in_scores, int32_t W,
     int64_t Q, int32_t k, int64_t rstride, int32_t* __restrict__ docs,
     float* __restrict__ scores) {
-  __shared__ uint64_t buf[4][kMergeSortedCap];
+  __shared__ uint64_t buf[kQW][kMergeSortedCap];
   const int wave = (int)(threadIdx.x >> 6);
-  const int64_t q = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t q = (int64_t)blockIdx.x * kQW + wave;
   if (q >= Q) return;  // wave-uniform; no barriers
   uint64_t* kb = buf[wave];
   const uint32_t lane = lane_id();
   const int n = W * k;
-  // staged with every load of the wave in flight (n <= 1024: 16 per lane)
   constexpr int U = kMergeSortedCap / 64;
   float sv[U];
   int32_t dv[U];
@@ -2438,34 +2455,27 @@ __global__ __launch_bounds__(256) void merge_sorted_kernel(
     const int w = i / k, j = i - w * k;
     const int64_t o = (int64_t)w * rstride + q * k + j;
     sv[u] = i < n ? in_scores[o] : 0.f;
-    dv[u] = i < n ? in_docs[o] : 0;
+    dv[u] = i < n ? in_docs[o] : -1;
   }
+  uint64_t key[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int i = u * 64 + (int)lane;
-    if (i < n) kb[i] = make_key(sv[u], (uint32_t)dv[u]);
+    key[u] = i < n ? make_key(sv[u], (uint32_t)dv[u]) : 0ull;  // (padding: key 0)
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  int pos = 0;
-  uint64_t head = ((int)lane < W) ? kb[lane * k] : 0ull;
-  for (int j = 0; j < k; ++j) {
-    const uint32_t hh = wave_max_u32((uint32_t)(head >> 32));
-    const uint32_t hl = wave_max_u32((uint32_t)(head >> 32) == hh ? (uint32_t)head : 0u);
-    const uint64_t best = ((uint64_t)hh << 32) | hl;
-    if (lane == 0) {
-      if (best == 0ull) {  // every list is down to its padding
-        docs[q * k + j] = -1;
-        scores[q * k + j] = __uint_as_float(0xFFFFFFFFu);
-      } else {
-        docs[q * k + j] = (int32_t)(0xFFFFFFFFu - (uint32_t)best);
-        scores[q * k + j] = key_score(hh);
-      }
-    }
-    if (best != 0ull && head == best) {
-      ++pos;
-      head = pos < k ? kb[lane * k + pos] : 0ull;
-    }
+  uint32_t kept = 0;
+  const uint64_t kth = wave_kth_key<U>(key, k, kept);
+  uint32_t base = 0u;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bool keep = key[u] != 0ull && key[u] >= kth;
+    const uint64_t b = __ballot(keep);
+    if (keep)
+      kb[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[u];
+    base += (uint32_t)__popcll(b);
   }
+  wave_sort_write(kb, kept, next_pow2(kept > 1u ? kept : 2u), k, 0, q, docs, scores);
 }
 
 // ---------------------------------------------------------------------------
@@ -2821,7 +2831,7 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
     sg.sample_stride = g.S;
   }
   if (!theta_ready)
-    hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, st,
+    hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + kQW - 1) / kQW)), dim3(64 * kQW), 0, st,
                        all_keys, (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt,
                        ws.list_cap, ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs, ws.counters);
   launch_phase<S_, kRest>(ix, q, T, Q, sg, ws, st);
@@ -2900,7 +2910,7 @@ static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k,
     // sampled main stage: one wavefront per query; the queries it leaves go
     // to the block merge below (their count on the device, usually 0)
     // (merge_tail_kernel takes the queries it leaves)
-    hipLaunchKernelGGL(merge_fast_kernel, dim3((unsigned)((sg.nq_host + 3) / 4)), dim3(256), 0,
+    hipLaunchKernelGGL(merge_fast_kernel, dim3((unsigned)((sg.nq_host + kQW - 1) / kQW)), dim3(64 * kQW), 0,
                        st, sg, (int32_t)k, ix.doc_offset, ws, docs, scores);
     return;
   }
@@ -2986,7 +2996,7 @@ hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores, int6
     return launch_merge_large(d_docs, d_scores, W, Q, k, rank_stride, d_out_docs, d_out_scores,
                               stream);
   if (sorted && W * k <= kMergeSortedCap && W <= 64) {
-    hipLaunchKernelGGL(merge_sorted_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, stream,
+    hipLaunchKernelGGL(merge_sorted_kernel, dim3((unsigned)((Q + kQW - 1) / kQW)), dim3(64 * kQW), 0, stream,
                        d_docs, d_scores, (int32_t)W, Q, (int32_t)k, rank_stride, d_out_docs,
                        d_out_scores);
     return hipGetLastError();
