@@ -162,6 +162,16 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
          (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+// Bitwise OR over the 64 lanes (DPP inside rows, then SGPRs); AND as ~OR(~x).
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) | (uint32_t)__builtin_amdgcn_readlane((int)v, 16) |
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 // Inclusive prefix sum over the wave.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   const int lane = lane_id();
@@ -1914,40 +1924,69 @@ __global__ __launch_bounds__(64 * kQW) void theta_wave_kernel(const uint64_t* __
         const uint32_t w = i / (uint32_t)S;
         key[j] = i < (uint32_t)n ? all_keys[((int64_t)w * Q + q) * S + (i - w * (uint32_t)S)] : 0ull;
       }
-      // score half first (32 steps on u32), then the doc half among the keys
-      // of that score — only when more than one key holds it (ties)
-      uint32_t hi = 0u;
-      for (int bit = 31; bit >= 0; --bit) {
-        const uint32_t hm = ~0u << bit, cand = hi | (1u << bit);
-        uint32_t c = 0;
+      // fewer than k real keys: the k-th is a zero key (no threshold)
+      uint32_t nz = 0u, om = 0u, nm = 0u;
 #pragma unroll
-        for (int j = 0; j < kThetaR; ++j) c += ((uint32_t)(key[j] >> 32) & hm) == cand;
-        const uint32_t tot = wave_sum_u32(c);
-        if (tot >= need) hi = cand;
-        else need -= tot;
-      }
-      uint32_t ties = 0;
-#pragma unroll
-      for (int j = 0; j < kThetaR; ++j) ties += (uint32_t)(key[j] >> 32) == hi;
-      uint32_t lo = 0u;
-      if (wave_sum_u32(ties) == 1u) {  // the one key of that score
-        uint32_t m = 0u;
-#pragma unroll
-        for (int j = 0; j < kThetaR; ++j) m = (uint32_t)(key[j] >> 32) == hi ? (uint32_t)key[j] : m;
-        lo = wave_max_u32(m);
-      } else {
+      for (int j = 0; j < kThetaR; ++j)
+        if (key[j] != 0ull) {
+          ++nz;
+          om |= (uint32_t)(key[j] >> 32);
+          nm |= ~(uint32_t)(key[j] >> 32);
+        }
+      if (wave_sum_u32(nz) >= (uint32_t)k) {
+        // score half first, then the doc half among the keys of that score —
+        // only when more than one key holds it (ties).  The k-th key is a real
+        // key: bits no real key sets stay 0, bits every real key sets are 1,
+        // and only the others take a counting step (tile-bound keys carry
+        // f16-valued scores: 13 mantissa bits are never set)
+        om = wave_or_u32(om);
+        const uint32_t am = ~wave_or_u32(nm);
+        uint32_t hi = 0u;
         for (int bit = 31; bit >= 0; --bit) {
-          const uint32_t hm = ~0u << bit, cand = lo | (1u << bit);
+          const uint32_t b1 = 1u << bit;
+          if (!(om & b1)) continue;  // (uniform)
+          if (am & b1) { hi |= b1; continue; }
+          const uint32_t hm = ~0u << bit, cand = hi | b1;
           uint32_t c = 0;
 #pragma unroll
-          for (int j = 0; j < kThetaR; ++j)
-            c += (uint32_t)(key[j] >> 32) == hi && ((uint32_t)key[j] & hm) == cand;
+          for (int j = 0; j < kThetaR; ++j) c += ((uint32_t)(key[j] >> 32) & hm) == cand;
           const uint32_t tot = wave_sum_u32(c);
-          if (tot >= need) lo = cand;
+          if (tot >= need) hi = cand;
           else need -= tot;
         }
+        uint32_t ties = 0, ol = 0u, nl = 0u;
+#pragma unroll
+        for (int j = 0; j < kThetaR; ++j)
+          if ((uint32_t)(key[j] >> 32) == hi) {
+            ++ties;
+            ol |= (uint32_t)key[j];
+            nl |= ~(uint32_t)key[j];
+          }
+        uint32_t lo = 0u;
+        if (wave_sum_u32(ties) == 1u) {  // the one key of that score
+          uint32_t m = 0u;
+#pragma unroll
+          for (int j = 0; j < kThetaR; ++j) m = (uint32_t)(key[j] >> 32) == hi ? (uint32_t)key[j] : m;
+          lo = wave_max_u32(m);
+        } else {
+          ol = wave_or_u32(ol);
+          const uint32_t al = ~wave_or_u32(nl);
+          for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t b1 = 1u << bit;
+            if (!(ol & b1)) continue;
+            if (al & b1) { lo |= b1; continue; }
+            const uint32_t hm = ~0u << bit, cand = lo | b1;
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < kThetaR; ++j)
+              c += (uint32_t)(key[j] >> 32) == hi && ((uint32_t)key[j] & hm) == cand;
+            const uint32_t tot = wave_sum_u32(c);
+            if (tot >= need) lo = cand;
+            else need -= tot;
+          }
+        }
+        prefix = ((uint64_t)hi << 32) | lo;
       }
-      prefix = ((uint64_t)hi << 32) | lo;
     } else {
       for (int bit = 63; bit >= 0; --bit) {
         const uint64_t hm = ~0ull << bit, cand = prefix | (1ull << bit);
@@ -2133,9 +2172,24 @@ __device__ __forceinline__ uint64_t wave_kth_key(const uint64_t (&key)[R], int32
   for (int j = 0; j < R; ++j) n += key[j] != 0ull;
   n = wave_sum_u32(n);
   if (n > (uint32_t)k) {
+    // bits no real key sets stay 0 and bits every real key sets are 1 in the
+    // answer (the k-th key is a real key): only the bits that differ need a
+    // counting step (f16-valued scores leave 13 mantissa bits unused)
+    uint32_t om = 0u, nm = 0u;  // OR and NOR-complement (~AND) over the real keys
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (key[j] != 0ull) {
+        om |= (uint32_t)(key[j] >> 32);
+        nm |= ~(uint32_t)(key[j] >> 32);
+      }
+    om = wave_or_u32(om);
+    const uint32_t am = ~wave_or_u32(nm);
     uint32_t need = (uint32_t)k, hi = 0u;
     for (int bit = 31; bit >= 0; --bit) {
-      const uint32_t hm = ~0u << bit, cand = hi | (1u << bit);
+      const uint32_t b1 = 1u << bit;
+      if (!(om & b1)) continue;         // (uniform)
+      if (am & b1) { hi |= b1; continue; }
+      const uint32_t hm = ~0u << bit, cand = hi | b1;
       uint32_t c = 0;
 #pragma unroll
       for (int j = 0; j < R; ++j) c += ((uint32_t)(key[j] >> 32) & hm) == cand;
@@ -2144,13 +2198,23 @@ __device__ __forceinline__ uint64_t wave_kth_key(const uint64_t (&key)[R], int32
       else need -= tot;
     }
     // need = rank of the answer among the keys of score hi
-    uint32_t ties = 0;
+    uint32_t ties = 0, ol = 0u, nl = 0u;
 #pragma unroll
-    for (int j = 0; j < R; ++j) ties += (uint32_t)(key[j] >> 32) == hi;
+    for (int j = 0; j < R; ++j)
+      if ((uint32_t)(key[j] >> 32) == hi) {
+        ++ties;
+        ol |= (uint32_t)key[j];
+        nl |= ~(uint32_t)key[j];
+      }
     uint32_t lo = 0u;
     if (wave_sum_u32(ties) > 1u) {
+      ol = wave_or_u32(ol);
+      const uint32_t al = ~wave_or_u32(nl);
       for (int bit = 31; bit >= 0; --bit) {
-        const uint32_t hm = ~0u << bit, cand = lo | (1u << bit);
+        const uint32_t b1 = 1u << bit;
+        if (!(ol & b1)) continue;
+        if (al & b1) { lo |= b1; continue; }
+        const uint32_t hm = ~0u << bit, cand = lo | b1;
         uint32_t c = 0;
 #pragma unroll
         for (int j = 0; j < R; ++j)
@@ -2435,6 +2499,36 @@ __global__ __launch_bounds__(kMergeNT) void merge_lists_kernel(
 // unique (global doc ids) except padding (0).
 constexpr int kMergeSortedCap = 1024;  // keys per wave
 
+// The cnt keys in the wave's LDS slice -> the best k of them, sorted and
+// written (global doc ids: no offset).  Every key is read into registers
+// before the slice is rewritten (one wave: its LDS operations keep order).
+template <int R>
+__device__ __forceinline__ void lds_merge_one(uint64_t* kb, uint32_t cnt, int32_t k, int64_t q,
+                                              int32_t* __restrict__ docs,
+                                              float* __restrict__ scores) {
+  const uint32_t lane = lane_id();
+  uint64_t key[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const uint32_t i = (uint32_t)j * 64u + lane;
+    key[j] = i < cnt ? kb[i] : 0ull;
+  }
+  uint32_t kept = 0;
+  const uint64_t kth = wave_kth_key<R>(key, k, kept);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  uint32_t base = 0u;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const bool keep = key[j] != 0ull && key[j] >= kth;
+    const uint64_t b = __ballot(keep);
+    if (keep)
+      kb[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
+    base += (uint32_t)__popcll(b);
+  }
+  wave_sort_write(kb, kept, next_pow2(kept > 1u ? kept : 2u), k, 0, q, docs, scores);
+}
+
 __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
     const int32_t* __restrict__ in_docs, const float* __restrict__ in_scores, int32_t W,
     int64_t Q, int32_t k, int64_t rstride, int32_t* __restrict__ docs,
@@ -2463,19 +2557,26 @@ __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
     const int i = u * 64 + (int)lane;
     key[u] = i < n ? make_key(sv[u], (uint32_t)dv[u]) : 0ull;  // (padding: key 0)
   }
-  uint32_t kept = 0;
-  const uint64_t kth = wave_kth_key<U>(key, k, kept);
-  uint32_t base = 0u;
+  // the lists' real keys (most slots are padding: the world holds ~2-3 k keys
+  // >= theta) compacted into LDS, then selected from the fewest registers
+  uint32_t cnt = 0u;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const bool keep = key[u] != 0ull && key[u] >= kth;
-    const uint64_t b = __ballot(keep);
-    if (keep)
-      kb[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[u];
-    base += (uint32_t)__popcll(b);
+    const bool nz = key[u] != 0ull;
+    const uint64_t b = __ballot(nz);
+    if (nz)
+      kb[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                         __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[u];
+    cnt += (uint32_t)__popcll(b);
   }
-  wave_sort_write(kb, kept, next_pow2(kept > 1u ? kept : 2u), k, 0, q, docs, scores);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const uint32_t nj = (cnt + 63u) >> 6;
+  if (nj <= 4u)
+    lds_merge_one<4>(kb, cnt, k, q, docs, scores);
+  else if (nj <= 8u)
+    lds_merge_one<8>(kb, cnt, k, q, docs, scores);
+  else
+    lds_merge_one<U>(kb, cnt, k, q, docs, scores);
 }
 
 // ---------------------------------------------------------------------------
