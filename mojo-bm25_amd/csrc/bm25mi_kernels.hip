@@ -2279,9 +2279,68 @@ __device__ __forceinline__ void wave_sort_write(uint64_t* keys, uint32_t n, int 
 // all keys at it compacted into the wave's LDS slice and sorted.  Returns
 // false (nothing written) when score ties make that more than kFastMaxK
 // keys: the block merge takes the query.
+template <int R>
+__device__ __forceinline__ void lds_merge_one(uint64_t* kb, uint32_t cnt, int32_t k,
+                                              int64_t doc_offset, int64_t q,
+                                              int32_t* __restrict__ docs,
+                                              float* __restrict__ scores);
+
+// First attempt for a long list: a provisional threshold from a sample of it
+// (every s-th key, <= 1024 in registers: the ceil(2k / s)-th best sample key,
+// expected ~2k list keys at or above it), one pass compacting the keys at or
+// above it into the wave's LDS slice, then the exact merge of those.  Valid
+// whenever they are at least k (the top k are among them) and fit the slice;
+// otherwise it returns false and the digit passes below run.
+__device__ bool long_merge_sampled(const Stage& sg, int32_t k, int64_t doc_offset, int64_t q,
+                                   int32_t cnt, uint64_t* keys, int32_t* __restrict__ docs,
+                                   float* __restrict__ scores) {
+  const uint32_t lane = lane_id();
+  const uint64_t* lst = sg.list + q * (int64_t)sg.C;
+  constexpr int RS = 16;
+  const int s = (cnt + 64 * RS - 1) / (64 * RS);  // sample stride
+  uint64_t smp[RS];
+#pragma unroll
+  for (int j = 0; j < RS; ++j) {
+    const int64_t i = (int64_t)(j * 64 + (int)lane) * s;
+    smp[j] = i < cnt ? lst[i] : 0ull;
+  }
+  const int32_t want = min((2 * k + s - 1) / s, 64 * RS);
+  uint32_t nk = 0;
+  const uint64_t t1 = wave_kth_key<RS>(smp, want, nk);  // (0: the sample holds fewer)
+  uint32_t base = 0u;
+  for (int i0 = 0; i0 < cnt; i0 += 8 * 64) {
+    uint64_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + (int)lane;
+      x[u] = i < cnt ? lst[i] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool keep = x[u] != 0ull && x[u] >= t1;
+      const uint64_t b = __ballot(keep);
+      const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+      if (keep && pos < (uint32_t)kFastMaxK) keys[pos] = x[u];
+      base += (uint32_t)__popcll(b);
+    }
+  }
+  if (base < (uint32_t)k || base > (uint32_t)kFastMaxK) return false;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const uint32_t nj = (base + 63u) >> 6;
+  if (nj <= 4u)
+    lds_merge_one<4>(keys, base, k, doc_offset, q, docs, scores);
+  else if (nj <= 8u)
+    lds_merge_one<8>(keys, base, k, doc_offset, q, docs, scores);
+  else
+    lds_merge_one<16>(keys, base, k, doc_offset, q, docs, scores);
+  return true;
+}
+
 __device__ bool long_merge_one(const Stage& sg, int32_t k, int64_t doc_offset, int64_t q,
                                int32_t cnt, uint64_t* keys, uint32_t* h,
                                int32_t* __restrict__ docs, float* __restrict__ scores) {
+  if (long_merge_sampled(sg, k, doc_offset, q, cnt, keys, docs, scores)) return true;
   const uint32_t lane = lane_id();
   const uint64_t* lst = sg.list + q * (int64_t)sg.C;
   uint32_t prefix = 0u, need = (uint32_t)k;
@@ -2503,7 +2562,8 @@ constexpr int kMergeSortedCap = 1024;  // keys per wave
 // written (global doc ids: no offset).  Every key is read into registers
 // before the slice is rewritten (one wave: its LDS operations keep order).
 template <int R>
-__device__ __forceinline__ void lds_merge_one(uint64_t* kb, uint32_t cnt, int32_t k, int64_t q,
+__device__ __forceinline__ void lds_merge_one(uint64_t* kb, uint32_t cnt, int32_t k,
+                                              int64_t doc_offset, int64_t q,
                                               int32_t* __restrict__ docs,
                                               float* __restrict__ scores) {
   const uint32_t lane = lane_id();
@@ -2526,7 +2586,7 @@ __device__ __forceinline__ void lds_merge_one(uint64_t* kb, uint32_t cnt, int32_
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
     base += (uint32_t)__popcll(b);
   }
-  wave_sort_write(kb, kept, next_pow2(kept > 1u ? kept : 2u), k, 0, q, docs, scores);
+  wave_sort_write(kb, kept, next_pow2(kept > 1u ? kept : 2u), k, doc_offset, q, docs, scores);
 }
 
 __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
@@ -2572,11 +2632,11 @@ __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const uint32_t nj = (cnt + 63u) >> 6;
   if (nj <= 4u)
-    lds_merge_one<4>(kb, cnt, k, q, docs, scores);
+    lds_merge_one<4>(kb, cnt, k, 0, q, docs, scores);
   else if (nj <= 8u)
-    lds_merge_one<8>(kb, cnt, k, q, docs, scores);
+    lds_merge_one<8>(kb, cnt, k, 0, q, docs, scores);
   else
-    lds_merge_one<U>(kb, cnt, k, q, docs, scores);
+    lds_merge_one<U>(kb, cnt, k, 0, q, docs, scores);
 }
 
 // ---------------------------------------------------------------------------
