@@ -207,8 +207,8 @@ int bm25_merge_sorted_device(int device, const int32_t* d_docs,
  *   bm25_sample_width(idx, shard_docs_max, world, k, &S): keys per query each
  *     rank samples (the same on every rank: shard_docs_max = the largest
  *     shard's document count; S = 0: shards too small to sample, or
- *     k > 4096 — then the finish half lists the shard's exact top-k; S =
- *     min(k, ceil(2k / world)) tile-bound keys with the theta_bound option);
+ *     k > 4096 — then the finish half lists the shard's exact top-k; the
+ *     same S serves the tile-bound threshold, whose keys need no sampling);
  *   bm25_search_sample_device(...): this shard's sample keys -> d_keys
  *     (u64 [Q][S], zero-padded: a SAMPLE pass, or — theta_bound — the best S
  *     tile-bound keys, read from the tile bounds without scoring);
