@@ -59,6 +59,23 @@ def algorithmic_bytes(indptr: np.ndarray, queries: np.ndarray, k: int) -> int:
     return total
 
 
+def query_postings(indptr: np.ndarray, queries: np.ndarray) -> int:
+    """Postings the batch reads query by query: sum over queries of the
+    distinct terms' document frequencies (the posting part of B(q))."""
+    df = np.diff(indptr)
+    return int(sum(int(df[np.unique(row[row >= 0])].sum()) for row in queries))
+
+
+def batch_distinct_postings(indptr: np.ndarray, queries: np.ndarray) -> int:
+    """Postings of the batch's DISTINCT terms (SURVEY.md:381, BASELINE.md:49):
+    what one read of every posting list the batch needs would move — the
+    floor under the per-query algorithmic bytes once L2/MALL reuse across the
+    batch's queries is perfect."""
+    df = np.diff(indptr)
+    t = np.unique(queries[queries >= 0])
+    return int(df[t].sum())
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -178,6 +195,11 @@ def main():
                          "two all-gathers); replica = every rank holds the whole index and "
                          "searches its Q/N slice of the batch, no collective (SURVEY.md §8(e) "
                          "comparison point)")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="N > 1 shard mode: pipeline each batch as this many row ranges over "
+                         "forks of the rank's index on their own streams (bm25mi.dist."
+                         "_search_parts): one part's collectives and merges overlap another's "
+                         "score pass")
     ap.add_argument("--replica-of", type=int, default=0,
                     help="replica mode at N=1: run rank 0's slice of an R-way replica job "
                          "(Q/R queries on the whole index) — the one-GPU proxy of the N=R line")
@@ -257,7 +279,7 @@ def main():
 
     def step():
         if world > 1 and not replica:  # global theta: RCCL all-gathers of sample keys and [Q, k] lists (bm25mi.dist)
-            sharded_search(index, dq, k, sdm, d_docs, d_scores, None, stream)
+            sharded_search(index, dq, k, sdm, d_docs, d_scores, None, stream, parts=args.parts)
         else:
             index.search_device(dq, k, d_docs, d_scores, stream)
 
@@ -282,6 +304,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     prof = index.profile_read()
     dispatch = index.last_dispatch()
+    stats = index.search_stats()  # the last timed search's selection counters
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     # end-to-end (N=1): the host-buffer entry point bm25_search — H2D of the
     # query batch, the search, D2H of the [Q, k] results — timed per call
@@ -328,6 +351,15 @@ def main():
     # an index that fits the 256 MB Infinity Cache (MALL) is not HBM-bound:
     # its rate is effective bandwidth over algorithmic bytes (config 2)
     mall = info["device_bytes"] < 256 * 2**20
+    # the bytes beside the algorithmic ones: what the
+    # tile-bound skip spared (the kernel never reads those postings, so the
+    # algorithmic rate is partly an effective rate), the batch's distinct
+    # posting bytes (the reuse floor) and the counter-measured bytes
+    skip_post = int(stats.get("bound_skipped_postings", 0))
+    n_post = query_postings(indptr, queries)
+    distinct = batch_distinct_postings(indptr, queries)
+    read_bytes = alg_bytes - 8 * skip_post
+    phys = (traffic.get("hbm_bytes_per_launch") / (kern_ms * 1e-3) / 1e9) if traffic else None
     from bm25mi import _capi
 
     if rank == 0:
@@ -363,7 +395,9 @@ def main():
                 "parallelism": (f"replica x{world} (whole index per GPU, batch split, no "
                                 "collective)" if replica else f"doc-shard x{world}" + (
                     f" + {'RCCL' if args.backend == 'nccl' else args.backend} all-gathers "
-                    "(sample keys, packed [Q, k] lists)" if world > 1 else "")),
+                    "(sample keys, packed [Q, k] lists)" + (
+                        f", batch pipelined as {args.parts} parts on forked contexts"
+                        if args.parts > 1 else "") if world > 1 else "")),
                 "score_kernels": sorted(dispatch["kernels"]),
                 "term_lanes": dispatch["term_lanes"],
                 "tiles_per_item": dispatch["band_tiles"],
@@ -386,6 +420,27 @@ def main():
                            "score_flat_kernel REST)"),
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
+                "achieved_kind": ("effective: algorithmic bytes (SURVEY.md §8(d)) over the pass "
+                                  "time, including postings the REST tile skip never reads"
+                                  if skip_post > 0 else
+                                  "algorithmic bytes (SURVEY.md §8(d)) over the pass time"),
+                "bound_skip": {"pairs": int(stats.get("bound_skipped_tiles", 0)),
+                               "postings": skip_post,
+                               "share_of_postings": round(skip_post / max(n_post, 1), 4),
+                               "read_bytes": read_bytes,
+                               "read_frac": round(read_bytes / (kern_ms * 1e-3) / 1e9
+                                                  / HBM_PEAK_GBPS, 4),
+                               "note": "postings of the (query, tile) pairs whose term-maxima "
+                                       "sum stayed below theta (last timed search); read_bytes "
+                                       "= algorithmic minus 8 B per skipped posting"},
+                "batch_distinct_bytes": {"postings": distinct, "at_6B": 6 * distinct,
+                                         "at_8B": 8 * distinct,
+                                         "reuse": round(n_post / max(distinct, 1), 2),
+                                         "note": "every distinct term of the batch read once: "
+                                                 "6 B/posting in this engine's layout (u16 slot "
+                                                 "+ f32), 8 B on disk"},
+                "physical_GBps": round(phys, 1) if phys else None,
+                "physical_frac": round(phys / HBM_PEAK_GBPS, 4) if phys else None,
                 "scope": ("rank 0's query slice" if replica else
                           "rank 0's shard" if world > 1 else "the whole index"),
                 "note": (f"index of {info['device_bytes'] / 2**20:.1f} MiB fits the 256 MB "

@@ -77,8 +77,22 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
                       const int32_t* indices, const float* data,
                       int64_t doc_offset, bm25_index** out);
 
-/* Release every device allocation and stream of the handle. */
+/* Release every device allocation and stream of the handle (the index
+ * arrays once no fork of the handle is left). */
 int bm25_index_destroy(bm25_index* idx);
+
+/*
+ * A second search context on the same device-resident index: it shares the
+ * CSC arrays, segment table and tile bounds of `base` (no copy) and has its
+ * own workspace, staging buffers, options (copied from base) and internal
+ * stream, so searches on base and on its forks may run concurrently on
+ * different streams (the doc-sharded search pipelines the parts of a batch
+ * this way: bm25mi.dist.sharded_search(parts=2)).  Each handle is destroyed
+ * on its own; the index arrays are released with the last one.
+ * Replaces no reference call: BM25v.search is stateless per call
+ * (bm25_native.py:76-158), which a fork per concurrent caller restores.
+ */
+int bm25_index_fork(bm25_index* base, bm25_index** out);
 
 /* Geometry of a built index (any pointer may be NULL). */
 int bm25_index_info(const bm25_index* idx, int64_t* n_docs, int64_t* n_terms,
@@ -287,11 +301,20 @@ int bm25_search_stats(bm25_index* idx, int64_t* rescored_tiles,
  * Any pointer may be NULL. */
 int bm25_search_stats_ex(bm25_index* idx, int64_t* rescored_tiles,
                          int64_t* fallback_queries, int64_t* bound_skipped);
+/* Every selection counter of the last search, the first n of (in order):
+ *   [0] tiles re-scored exactly, [1] queries sent to the exact fallback
+ *   stage, [2] (query, tile) pairs the REST pass skipped by their tile
+ *   bound, [3] the postings of those skipped (query, tile) segments (what
+ *   the skip saved of the algorithmic bytes, 8 B each), [4] queries left to
+ *   the block merge (lists longer than one wavefront's registers).
+ * n must be in 1..5. */
+int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
 
 /*
  * Search options of one handle.  A new handle takes them from the
  * environment (BM25_FLAT, BM25_FLAT_BW, BM25_ITEMS_PER_WAVE, BM25_SAMPLE_P,
- * BM25_LIST_CAP, BM25_CLAIM_CH, BM25_CLAIM_M, BM25_TILE_BOUND, BM25_THETA_BOUND) at
+ * BM25_LIST_CAP, BM25_CLAIM_CH, BM25_CLAIM_M, BM25_TILE_BOUND, BM25_THETA_BOUND,
+ * BM25_GRID_PCT) at
  * bm25_index_create; these
  * calls change or read them afterwards, effective from the next search.
  * Results never depend on them (every setting is bit-exact); they choose
@@ -316,6 +339,10 @@ int bm25_search_stats_ex(bm25_index* idx, int64_t* rescored_tiles,
  *                    document's score lower bound) with no SAMPLE pass;
  *                    0: the sampled threshold.  Every shard of a multi-rank
  *                    search needs the same setting (bm25_sample_width)
+ *   "grid_pct"       percent of the device's resident workgroup slots the
+ *                    persistent score kernels launch (1..100, default 100):
+ *                    below 100 leaves slots for kernels of another stream
+ *                    (a concurrent search on a fork, the collectives)
  * Replaces no reference call (the reference has no tuning surface; its MAX
  * custom op takes compile-time parameters, graph.py:72).
  */

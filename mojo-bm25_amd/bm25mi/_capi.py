@@ -50,6 +50,7 @@ _SIGS = {
     "bm25_index_create": ([ctypes.c_int, _I64, _I64, _I64, _P, ctypes.c_int, _P, _P, _I64,
                            ctypes.POINTER(_P)], ctypes.c_int),
     "bm25_index_destroy": ([_P], ctypes.c_int),
+    "bm25_index_fork": ([_P, ctypes.POINTER(_P)], ctypes.c_int),
     "bm25_index_info": ([_P, _PI64, _PI64, _PI64, _PI32, _PI64, _PI64], ctypes.c_int),
     "bm25_index_segments": ([_P, _PI32, _PI64], ctypes.c_int),
     "bm25_index_bounds": ([_P, _PI32, _PI64], ctypes.c_int),
@@ -65,6 +66,7 @@ _SIGS = {
     "bm25_profile_read": ([_P, _PD, _PI64, _PD, _PI64, _PI64], ctypes.c_int),
     "bm25_search_stats": ([_P, _PI64, _PI64], ctypes.c_int),
     "bm25_search_stats_ex": ([_P, _PI64, _PI64, _PI64], ctypes.c_int),
+    "bm25_search_counters": ([_P, _PI64, _I32], ctypes.c_int),
     "bm25_index_set_option": ([_P, ctypes.c_char_p, _I64], ctypes.c_int),
     "bm25_index_get_option": ([_P, ctypes.c_char_p, _PI64], ctypes.c_int),
     "bm25_search_dispatch": ([_P, ctypes.POINTER(ctypes.c_uint32), _PI32, _PI32, _PI32],

@@ -101,7 +101,8 @@ def _agree_width(index, S: int, k: int, device, group=None) -> None:
     ``theta_bound`` options (and on the shard having tile bounds), which each
     rank sets on its own.  Checked once per (group, k) by one
     all-reduce of (S, -S) with MAX; every rank raises the same ValueError when
-    they differ."""
+    they differ.  GpuIndex.set_option drops the cache, so a changed option
+    is re-checked on the next search — every rank must change it together."""
     seen = index.__dict__.setdefault("_bm25_width_ok", set())
     key = (_group_key(group), int(k))
     if key in seen:
@@ -122,12 +123,95 @@ def gather_keys(keys: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -
     return _all_gather(keys, group)
 
 
+def _forks(index, parts: int):
+    """The index and parts - 1 forks of it (bm25_index_fork: shared device
+    arrays, own workspaces), created once and cached on the index.  Options
+    are copied at fork time; set_option on the index drops the cache."""
+    forks = index.__dict__.setdefault("_bm25_forks", [])
+    while len(forks) < parts - 1:
+        forks.append(index.fork())
+    return [index] + forks[:parts - 1]
+
+
+def _part_streams(index, parts: int, device):
+    """One torch stream per part (cached on the index), or None on the CPU."""
+    if device.type != "cuda":
+        return [None] * parts
+    st = index.__dict__.setdefault("_bm25_part_streams", [])
+    while len(st) < parts:
+        st.append(torch.cuda.Stream(device=device))
+    return st[:parts]
+
+
+def _stream_ctx(s):
+    import contextlib
+    return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
+
+
+def _search_parts(index, d_queries, k, shard_docs_max, d_docs, d_scores, stream, group, world,
+                  S, parts):
+    """sharded_search over `parts` contiguous row ranges of the batch, each
+    on its own fork of the index and its own stream, issued phase by phase
+    (every part's sample half, every part's key all-gather, every finish
+    half, every list all-gather, every W-way merge).  The device then runs one
+    part's collectives and its latency-bound kernels (threshold, merges: one
+    wavefront per query) beside another part's score pass — the per-batch
+    fixed costs of a doc shard overlap instead of adding up.
+    Collectives keep one issue order on every rank.  The result is the
+    unsplit search's, row for row."""
+    from .index import merge_sorted_device
+    Q = d_queries.shape[0]
+    cuts = [Q * i // parts for i in range(parts + 1)]
+    rows = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    ctxs = _forks(index, len(rows))
+    dev = d_queries.device
+    streams = _part_streams(index, len(rows), dev)
+    if streams[0] is not None:  # the parts start after the caller's stream
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        for s in streams:
+            s.wait_event(ev)
+    qs = [d_queries[a:b] for a, b in rows]
+    keys, all_keys, packed, gathered = [], [], [], []
+    for i, (a, b) in enumerate(rows):
+        with _stream_ctx(streams[i]):
+            kk = (torch.empty if S > 0 else torch.zeros)((b - a, max(S, 1)), dtype=torch.int64,
+                                                        device=dev)
+            if S > 0:
+                ctxs[i].search_sample_device(qs[i], k, world, shard_docs_max, kk, streams[i])
+            keys.append(kk)
+    for i in range(len(rows)):
+        with _stream_ctx(streams[i]):
+            all_keys.append(gather_keys(keys[i], group) if world > 1 and S > 0
+                            else keys[i].unsqueeze(0))
+    for i, (a, b) in enumerate(rows):
+        with _stream_ctx(streams[i]):
+            pk = torch.empty((2, b - a, k), dtype=torch.int32, device=dev)
+            ctxs[i].search_finish_device(qs[i], k, world, shard_docs_max, all_keys[i], pk[0],
+                                         pk[1].view(torch.float32), streams[i])
+            packed.append(pk)
+    for i in range(len(rows)):
+        with _stream_ctx(streams[i]):
+            gathered.append(_all_gather(packed[i], group) if world > 1 else packed[i].unsqueeze(0))
+    for i, (a, b) in enumerate(rows):
+        with _stream_ctx(streams[i]):
+            g = gathered[i]
+            merge_sorted_device(dev.index, g, g[:, 1].view(torch.float32), world, b - a, k,
+                                2 * (b - a) * k, d_docs[a:b], d_scores[a:b], streams[i])
+    if streams[0] is not None:  # the caller's stream continues after every part
+        for s in streams:
+            ev = torch.cuda.Event()
+            ev.record(s)
+            stream.wait_event(ev)
+    return d_docs, d_scores
+
+
 def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
                    d_docs: torch.Tensor, d_scores: torch.Tensor,
                    merge: Optional[MergeFn] = None, stream=None,
                    group: Optional[dist.ProcessGroup] = None,
                    exchange: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
-                   n_docs_total: Optional[int] = None
+                   n_docs_total: Optional[int] = None, parts: int = 1
                    ) -> Tuple[torch.Tensor, torch.Tensor]:
     """One rank's doc-sharded search with a GLOBAL threshold (bm25_search_
     sample/finish_device): this shard's sample keys are all-gathered, theta =
@@ -147,7 +231,11 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
     ``k`` is checked against the whole collection's document count, as the
     single-index search checks it (numpy's argpartition error,
     bm25_native.py:205): ``n_docs_total``, or one all-reduce of the shards'
-    counts on the first search (cached on ``index``)."""
+    counts on the first search (cached on ``index``).
+
+    ``parts`` > 1 (packed lists, no ``merge`` / ``exchange``): the batch's
+    rows are searched as that many parts pipelined over forks of the index
+    on their own streams (``_search_parts``) — the same result."""
     world = int(exchange.world) if exchange is not None else dist.get_world_size(group)
     total = n_docs_total if n_docs_total is not None else (
         _global_docs(index, d_queries.device, group) if exchange is None else None)
@@ -157,10 +245,18 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
     S = index.sample_width(k, world, shard_docs_max)
     if exchange is None and world > 1:
         _agree_width(index, S, k, d_queries.device, group)
-    if stream is None:
+    cuda = d_queries.device.type == "cuda"
+    if not cuda:
+        stream = None
+    elif stream is None:
         stream = torch.cuda.current_stream(d_queries.device)
     elif not isinstance(stream, torch.cuda.Stream):
         stream = torch.cuda.ExternalStream(int(stream), device=d_queries.device)
+    if parts > 1 and merge is None and exchange is None:
+        return _search_parts(index, d_queries, k, shard_docs_max, d_docs, d_scores, stream,
+                             group, world, S, parts)
+    if not cuda:
+        raise ValueError("sharded_search runs on the GPU (parts > 1 for CPU protocol tests)")
     with torch.cuda.stream(stream):
         Q = d_queries.shape[0]
         # S > 0: the sample pass writes every key of its own width

@@ -69,6 +69,18 @@ class GpuIndex:
             m.sum_duplicates()
         return cls(m.indptr, m.indices, m.data, m.shape[0], device=device, doc_offset=doc_offset)
 
+    def fork(self) -> "GpuIndex":
+        """Another search context on the same device arrays (bm25_index_fork):
+        its own workspace, options (copied) and stream, so searches on this
+        handle and on the fork may run concurrently on different streams."""
+        h = ctypes.c_void_p()
+        check(lib.bm25_index_fork(self._h, ctypes.byref(h)))
+        g = GpuIndex.__new__(GpuIndex)
+        g.__dict__.update({k: v for k, v in self.__dict__.items() if not k.startswith("_")})
+        g._indptr = g._indices = g._data = None
+        g._h = h
+        return g
+
     # ------------------------------------------------------------------
     def close(self) -> None:
         if self._h is not None:
@@ -195,8 +207,13 @@ class GpuIndex:
     def set_option(self, name: str, value: int) -> None:
         """A search option of this handle (bm25_index_set_option: flat,
         flat_bw, items_per_wave, sample_p, list_cap, claim_ch, claim_m,
-        tile_bound, theta_bound)."""
+        tile_bound, theta_bound).  In a multi-rank search every rank must
+        change an option together (like a collective): the next
+        ``bm25mi.dist.sharded_search`` re-checks the sample width they agree on."""
         check(lib.bm25_index_set_option(self._h, name.encode(), int(value)))
+        self.__dict__.pop("_bm25_width_ok", None)  # (bm25mi.dist._agree_width's cache)
+        for f in self.__dict__.get("_bm25_forks", []):  # (bm25mi.dist's part contexts)
+            f.set_option(name, value)
 
     def get_option(self, name: str) -> int:
         v = ctypes.c_int64()
@@ -222,15 +239,15 @@ class GpuIndex:
                 "sample_p": sp_.value}
 
     def search_stats(self) -> dict:
-        """Selection statistics of the last search: tiles re-scored exactly,
-        queries sent to the exact fallback stage, (query, tile) pairs the REST
-        pass skipped by their tile bound."""
-        r = ctypes.c_int64()
-        f = ctypes.c_int64()
-        b = ctypes.c_int64()
-        check(lib.bm25_search_stats_ex(self._h, ctypes.byref(r), ctypes.byref(f), ctypes.byref(b)))
-        return {"rescored_tiles": r.value, "fallback_queries": f.value,
-                "bound_skipped_tiles": b.value}
+        """Selection statistics of the last search (bm25_search_counters):
+        tiles re-scored exactly, queries sent to the exact fallback stage,
+        (query, tile) pairs the REST pass skipped by their tile bound and the
+        postings of those pairs, queries left to the block merge."""
+        v = (ctypes.c_int64 * 5)()
+        check(lib.bm25_search_counters(self._h, v, 5))
+        return {"rescored_tiles": v[0], "fallback_queries": v[1],
+                "bound_skipped_tiles": v[2], "bound_skipped_postings": v[3],
+                "block_merge_queries": v[4]}
 
 
 def merge_topk_device(device: int, d_docs, d_scores, W: int, Q: int, k: int, d_out_docs,

@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -54,10 +55,22 @@ struct EventPair {
   hipEvent_t a = nullptr, b = nullptr, c = nullptr;  // start, after score pass, end
 };
 
+// The device arrays of one built index, shared by the handle that built it
+// and its forks (bm25_index_fork): freed when the last of them is destroyed.
+struct IndexArrays {
+  int device = 0;
+  std::vector<void*> p;
+  ~IndexArrays() {
+    hipSetDevice(device);
+    for (void* x : p) hipFree(x);
+  }
+};
+
 }  // namespace
 
 struct bm25_index {
   DevIndex ix;
+  std::shared_ptr<IndexArrays> arrays;  // owner of ix's device arrays (null while building)
   hipStream_t stream = nullptr;
   Workspace ws;
   // host-call staging buffers (device)
@@ -119,6 +132,7 @@ SearchOpts env_opts() {
   o.claim_m = env_int("BM25_CLAIM_M", o.claim_m);
   o.tile_bound = env_int("BM25_TILE_BOUND", o.tile_bound) != 0;
   o.theta_bound = env_int("BM25_THETA_BOUND", o.theta_bound) != 0;
+  o.grid_pct = std::min(100, std::max(1, env_int("BM25_GRID_PCT", o.grid_pct)));
   return o;
 }
 
@@ -154,6 +168,9 @@ int set_opt(SearchOpts& o, const char* name, int64_t v) {
   } else if (n == "theta_bound") {
     if (v != 0 && v != 1) return fail(BM25_EINVAL, "theta_bound must be 0 or 1");
     o.theta_bound = (int)v;
+  } else if (n == "grid_pct") {
+    if (v < 1 || v > 100) return fail(BM25_EINVAL, "grid_pct must be in 1..100");
+    o.grid_pct = (int)v;
   } else {
     return fail(BM25_EINVAL, "unknown option '%s'", name);
   }
@@ -172,6 +189,7 @@ int get_opt(const SearchOpts& o, const char* name, int64_t* v) {
   else if (n == "claim_m") *v = o.claim_m;
   else if (n == "tile_bound") *v = o.tile_bound;
   else if (n == "theta_bound") *v = o.theta_bound;
+  else if (n == "grid_pct") *v = o.grid_pct;
   else return fail(BM25_EINVAL, "unknown option '%s'", name);
   return BM25_OK;
 }
@@ -287,6 +305,10 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   if (Q == 0 || k == 0) return BM25_OK;
   if (k > kMaxK) {  // any k up to n_docs: the large-k path (bm25mi_large.hip)
     HIP_TRY(order_ws(h, st), "workspace order");
+    // this search selects without the counters: the stats read as zero, not
+    // as the previous search's
+    if (h->ws.counters)
+      HIP_TRY(hipMemsetAsync(h->ws.counters, 0, sizeof(int32_t) * kCounters, st), "hipMemsetAsync");
     h->ix.disp = Dispatch{};
     h->ix.disp.sample_p = 1;
     EventPair* ev = next_events(h);
@@ -504,6 +526,9 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     return cleanup(fail(BM25_EINVAL,
                         "indices must be sorted, unique and in [0, n_docs) within every column "
                         "(canonical CSC)"));
+  h->arrays = std::make_shared<IndexArrays>();
+  h->arrays->device = device;
+  h->arrays->p = {ix.indptr, ix.rel, ix.tl_ptr, ix.tl_tile, ix.tl_start, ix.ldoc, ix.val, ix.bmax};
   *out = h;
   return cleanup(BM25_OK);
 }
@@ -512,6 +537,7 @@ int bm25_index_destroy(bm25_index* h) {
   if (!h) return BM25_OK;
   hipSetDevice(h->ix.device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->ws_done) hipEventSynchronize(h->ws_done);  // a search on a caller's stream
   for (auto& p : h->ev_pool) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
@@ -523,16 +549,36 @@ int bm25_index_destroy(bm25_index* h) {
   hipFree(h->d_docs);
   hipFree(h->d_scores);
   hipFree(h->d_maxtok);
-  hipFree(h->ix.indptr);
-  hipFree(h->ix.rel);
-  hipFree(h->ix.tl_ptr);
-  hipFree(h->ix.tl_tile);
-  hipFree(h->ix.tl_start);
-  hipFree(h->ix.ldoc);
-  hipFree(h->ix.val);
-  hipFree(h->ix.bmax);
+  if (h->arrays) {
+    h->arrays.reset();  // the index arrays go with the last handle sharing them
+  } else {              // a create that failed part-way
+    for (void* x : {(void*)h->ix.indptr, (void*)h->ix.rel, (void*)h->ix.tl_ptr,
+                    (void*)h->ix.tl_tile, (void*)h->ix.tl_start, (void*)h->ix.ldoc,
+                    (void*)h->ix.val, (void*)h->ix.bmax})
+      hipFree(x);
+  }
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
+  return BM25_OK;
+}
+
+int bm25_index_fork(bm25_index* base, bm25_index** out) {
+  if (!out) return fail(BM25_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!base || !base->arrays) return fail(BM25_EINVAL, "NULL or unbuilt index");
+  std::lock_guard<std::mutex> lk(base->mu);
+  HIP_TRY(hipSetDevice(base->ix.device), "hipSetDevice");
+  bm25_index* h = new bm25_index();
+  h->ix = base->ix;  // the same device arrays and options; its own dispatch report
+  h->ix.disp = Dispatch{};
+  h->arrays = base->arrays;
+  h->device_bytes = base->device_bytes;
+  const hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    bm25_index_destroy(h);
+    return hip_fail(e, "hipStreamCreate");
+  }
+  *out = h;
   return BM25_OK;
 }
 
@@ -876,6 +922,20 @@ int bm25_search_stats_ex(bm25_index* h, int64_t* rescored_tiles, int64_t* fallba
   if (rescored_tiles) *rescored_tiles = cnt[3];
   if (fallback_queries) *fallback_queries = cnt[2];
   if (bound_skipped) *bound_skipped = cnt[5];
+  return BM25_OK;
+}
+
+int bm25_search_counters(bm25_index* h, int64_t* out, int32_t n) {
+  if (!h || !out) return fail(BM25_EINVAL, "NULL argument");
+  if (n < 1 || n > 5) return fail(BM25_EINVAL, "n=%d must be in 1..5", n);
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  int32_t cnt[kCounters] = {};
+  read_counters(h, cnt);
+  uint64_t post = 0;
+  std::memcpy(&post, cnt + 6, sizeof post);  // counters[6..7]: a u64 (score_flat_kernel)
+  const int64_t v[5] = {cnt[3], cnt[2], cnt[5], (int64_t)post, cnt[4]};
+  for (int i = 0; i < n; ++i) out[i] = v[i];
   return BM25_OK;
 }
 

@@ -75,6 +75,7 @@ struct SearchOpts {
   int tile_bound = 1;      // REST skips tiles whose term-maxima sum is below theta (needs bmax)
   int theta_bound = 1;     // threshold keys from the tile bounds instead of a SAMPLE pass
                            // (needs bmax; search_geom)
+  int grid_pct = 100;      // percent of the resident slots the persistent score kernels take
 };
 
 // What the last search launched (bm25_search_dispatch).
@@ -141,7 +142,8 @@ struct Workspace {
   int32_t* counters = nullptr;   // [kCounters]: [0]/[1] rescore queue length / pop cursor,
                                  // [2] fallback queries, [3] tiles re-scored this search,
                                  // [4] queries left to the block merge (slow),
-                                 // [5] (query, tile) pairs REST skipped by their tile bound
+                                 // [5] (query, tile) pairs REST skipped by their tile bound,
+                                 // [6..7] (a u64) the postings of those pairs
   int32_t* slow = nullptr;       // [Q] those queries
   int32_t* wctr = nullptr;       // [kWctrRegions][kWctrInts] item-claim counters: zeroed once
                                  // at allocation; the last wave of each counter's sharers

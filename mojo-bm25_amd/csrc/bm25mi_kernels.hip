@@ -1020,6 +1020,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   };
 
   uint32_t nbound = 0;  // REST: (query, tile) pairs this lane's tiles skipped by their bound
+  uint32_t npost = 0;   // ... and the postings of this lane's skipped segments
   // ---- the issue side's item: its segments (lane s = tile * TT + term) and
   // row numbering; the item prefetch pipeline one and two items ahead
   uint32_t iSb = 0, iSl = 0, iIncl = 0, iExcl = 0;
@@ -1048,6 +1049,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
         for (int o = 1; o < (int)TT; o <<= 1) ub += __shfl_xor(ub, o, 64);
         const bool cut = ub * 1.0001f < key_score((uint32_t)(thN >> 32));
         if (cut && !skip && lt == 0u && (int)li < nx.bw) ++nbound;
+        // ... and their postings (lanes outside the item hold r1 == r0)
+        if (cut && !skip) npost += dN.r1 - dN.r0;
         skip = skip || cut;
       }
     }
@@ -1256,9 +1259,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     for (int s = 0; s < kFR; ++s) step(s);
   }
   if (curTi != kNoTile) epilogue();
-  if (PH == kRest && stats != nullptr) {  // bound-skipped tiles of this wave
+  if (PH == kRest && stats != nullptr) {  // bound-skipped tiles (and postings) of this wave
     const uint32_t nb = wave_sum_u32(nbound);
     if (lane == 0 && nb != 0u) atomicAdd(stats, (int32_t)nb);
+    // stats + 1 .. + 2: a u64 count (Workspace::counters[6..7], 8-B aligned)
+    const uint32_t np = wave_sum_u32(npost);
+    if (lane == 0 && np != 0u)
+      atomicAdd(reinterpret_cast<unsigned long long*>(stats + 1), (unsigned long long)np);
   }
   // every claim of this wave has returned (the last one, read by next(), ran
   // out of items) before it counts itself finished
@@ -2792,6 +2799,9 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
   const int64_t nt = PH == kSample ? sample_count(ix.ntiles, sg.P, sg.G) : ix.ntiles;
   auto go = [&](auto kern) {
     int grid = persistent_grid(kern, 64);
+    // grid_pct < 100: leave resident slots to another stream's kernels (whole
+    // XCD rounds: the item ranges are split over blockIdx % 8)
+    if (ix.opt.grid_pct < 100) grid = std::max(8, grid * ix.opt.grid_pct / 100 / 8 * 8);
     if (sg.nq_dev) grid = std::min(grid, 8 * kFallbackBlocks);  // fallback: usually no queries
     // every claim counter of an XCD range needs a wave: counter cm is served
     // by the workgroups with (blockIdx / 8) % claim_m == cm

@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round-5 GPU steps (outputs under gpurun_out/$NAME/); each GPU step has its
+# own time limit and the chain stops at the first failure.
+#   STEPS=tests   pytest -m gpu + smoke
+#   STEPS=lines   bench lines: c3 (CPU legs), c2 (CPU legs), replica proxy
+#                 (rank 0 of 8), c3 at k=10000 (large-k path), c3 at 16
+#                 terms, c5 (one rank's shard)
+#   STEPS=probe   scripts/shard_probe.py (W = PROBE_WS)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+NAME=${NAME:-r5}
+OUT=$R/gpurun_out/$NAME
+mkdir -p $OUT
+cd $R
+for step in ${STEPS:-tests lines}; do
+  case $step in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+    tail -1 $OUT/pytest_gpu.log
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; tail -20 $OUT/smoke.log; exit 1; }
+    ;;
+  c3)  # the headline line only
+    timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -20 $OUT/bench.err; exit 1; }
+    cat $OUT/bench.json
+    ;;
+  lines)
+    timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -20 $OUT/bench.err; exit 1; }
+    cat $OUT/bench.json
+    timeout -k 10 300 python -u bench.py --config c2 > $OUT/bench_c2.json 2> $OUT/bench_c2.err || { echo bench c2 failed; tail -20 $OUT/bench_c2.err; exit 1; }
+    timeout -k 10 300 python -u bench.py --replica-of 8 --cpu-queries 0 > $OUT/bench_replica8.json 2> $OUT/bench_replica8.err || { echo bench replica failed; tail -20 $OUT/bench_replica8.err; exit 1; }
+    timeout -k 10 300 python -u bench.py --k 10000 --steps 5 --warmup 2 --cpu-queries 0 --e2e-batches 0 > $OUT/bench_k10000.json 2> $OUT/bench_k10000.err || { echo bench k10000 failed; tail -20 $OUT/bench_k10000.err; exit 1; }
+    timeout -k 10 300 python -u bench.py --terms 16 --cpu-queries 0 > $OUT/bench_t16.json 2> $OUT/bench_t16.err || { echo bench t16 failed; tail -20 $OUT/bench_t16.err; exit 1; }
+    timeout -k 10 600 python -u bench.py --config c5 --cpu-queries 0 --e2e-batches 5 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { echo bench c5 failed; tail -20 $OUT/bench_c5.err; exit 1; }
+    ;;
+  variants)  # VLIBS: variant libraries timed against the product (scripts/variant_lib_time.py)
+    for cfg in ${VCFGS:-c3}; do
+      VCFG=${cfg%%:*} VTERMS=$([ "${cfg#*:}" != "$cfg" ] && echo ${cfg#*:}) timeout -k 10 900 python -u scripts/variant_lib_time.py $VLIBS > $OUT/variants_${cfg/:/_t}.jsonl 2> $OUT/variants_${cfg/:/_t}.err || { echo variants failed; tail -20 $OUT/variants_${cfg/:/_t}.err; exit 1; }
+      cat $OUT/variants_${cfg/:/_t}.jsonl
+    done
+    ;;
+  probe)  # per-rank config-3 shard work with real sample keys + modelled collectives
+    timeout -k 10 900 python -u scripts/shard_probe.py ${PROBE_WS:-1 2 4 8} > $OUT/shard_probe.jsonl 2> $OUT/shard_probe.err || { echo probe failed; tail -20 $OUT/shard_probe.err; exit 1; }
+    cat $OUT/shard_probe.jsonl
+    ;;
+  esac
+done
+exit 0

@@ -8,17 +8,27 @@ that stack, and the W lists are packed [W, 2, Q, k] as the list all-gather
 would deliver them.  The timed loop is then exactly one rank's batch: SAMPLE
 (its own slot of the stack rewritten, as the gather would), finish (theta over
 the WHOLE real sample, REST, list into its own slot of the packed buffer) and
-the W-way merge of the packed lists -- everything but the two collectives.  It
-is timed for every rank; the bench's step is the max over ranks.
+the W-way merge of the packed lists.  It is timed for every rank; the bench's
+step is the max over ranks.
 
 The two all-gathers are modelled, not measured (no multi-GPU box here):
-  t(bytes per rank) = ALPHA + bytes * (W - 1) / (LINKS_USED * LINK_GBS)
+  t(bytes per rank) = ALPHA + bytes / LINK_GBS
 with RCCL's direct all-gather over the point-to-point xGMI mesh: each rank's
 block goes to its W - 1 peers over W - 1 distinct links in parallel.  The
-constants are stated in the output line.
+constants are stated in the output line.  Two ways to add them:
+  * "serial": the modelled time added to the measured batch (no overlap);
+  * "inline" (PROBE_PARTS): each all-gather is a spin kernel of the modelled
+    duration (torch.cuda._sleep, calibrated) on ONE communication stream —
+    ProcessGroupNCCL's single stream per device — ordered between the part's
+    halves by events exactly as bm25mi.dist._search_parts orders the real
+    collectives.  With P parts on forks of the shard and their own streams,
+    one part's collectives and its one-wavefront-per-query kernels overlap
+    another part's REST pass; the step is measured with them in place.
 
   python scripts/shard_probe.py [W ...]     (env VLIB: a variant library;
-                                             PROBE_Q: batch size; PROBE_RANKS, PROBE_ITERS)
+      PROBE_Q: batch size; PROBE_RANKS, PROBE_ITERS; PROBE_PARTS: e.g. "1,2,4";
+      PROBE_GRID: grid_pct values, e.g. "100,90"; PROBE_HYBRID=1: also the
+      2-replica x W/2-shard split, each rank Q/2 queries on a 2/W shard)
 """
 import json
 import os
@@ -46,17 +56,88 @@ def model_gather_us(bytes_per_rank: int, W: int) -> float:
     return ALPHA_US + bytes_per_rank / (LINK_GBS * 1e3)
 
 
+_CYC_PER_US = None
+
+
+def sleep_us(us: float, stream) -> None:
+    """A spin kernel of ~us microseconds on `stream` (torch.cuda._sleep)."""
+    global _CYC_PER_US
+    if us <= 0:
+        return
+    if _CYC_PER_US is None:  # calibrate once: cycles of the spin per microsecond
+        s = torch.cuda.Stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(1000)
+            e0.record(s)
+            torch.cuda._sleep(2_000_000)
+            e1.record(s)
+        torch.cuda.synchronize()
+        _CYC_PER_US = 2_000_000 / (e0.elapsed_time(e1) * 1e3)
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(max(1, int(us * _CYC_PER_US)))
+
+
+def rank_parts(shards, r, q, k, W, smax, keys_p, g_p, rows, out_d, out_s, forks, streams, comm,
+               keys_us, list_us):
+    """One rank's batch as len(rows) parts (bm25mi.dist._search_parts with
+    modelled collectives inline on the `comm` stream)."""
+    dev = q.device.index
+    main = torch.cuda.current_stream()
+    ev = torch.cuda.Event()
+    ev.record(main)
+    ctx = [shards[r]] + forks
+    for s in streams:
+        s.wait_event(ev)
+
+    def coll(i, us):  # part i's collective: comm after part i's stream, part i after comm
+        e = torch.cuda.Event()
+        e.record(streams[i])
+        comm.wait_event(e)
+        sleep_us(us, comm)
+        e2 = torch.cuda.Event()
+        e2.record(comm)
+        streams[i].wait_event(e2)
+
+    for i, (a, b) in enumerate(rows):
+        ctx[i].search_sample_device(q[a:b], k, W, smax, keys_p[i][r], streams[i])
+    for i in range(len(rows)):
+        coll(i, keys_us)
+    for i, (a, b) in enumerate(rows):
+        g = g_p[i]
+        ctx[i].search_finish_device(q[a:b], k, W, smax, keys_p[i], g[r, 0],
+                                    g[r, 1].view(torch.float32), streams[i])
+    for i in range(len(rows)):
+        coll(i, list_us)
+    for i, (a, b) in enumerate(rows):
+        g = g_p[i]
+        merge_sorted_device(dev, g, g[:, 1].view(torch.float32), W, b - a, k, 2 * (b - a) * k,
+                            out_d[a:b], out_s[a:b], streams[i])
+    for s in streams:
+        e = torch.cuda.Event()
+        e.record(s)
+        main.wait_event(e)
+
+
 def main():
     cfg = synth.CONFIGS["c3"]
     nq = int(os.environ.get("PROBE_Q", "0")) or None  # batch size (default: the config's 1024)
-    q = torch.from_numpy(synth.make_queries(cfg, n_queries=nq)).cuda()
-    Q, k = q.shape[0], cfg.k
-    dev = q.device.index
+    q_full = torch.from_numpy(synth.make_queries(cfg, n_queries=nq)).cuda()
+    k = cfg.k
     st = torch.cuda.current_stream()
     n = int(os.environ.get("PROBE_ITERS", "10"))
     ranks_env = os.environ.get("PROBE_RANKS")
+    parts_list = [int(x) for x in os.environ.get("PROBE_PARTS", "1").split(",")]
+    grids = [int(x) for x in os.environ.get("PROBE_GRID", "100").split(",")]
+    hybrid = os.environ.get("PROBE_HYBRID") == "1"
     w1_ms = None
-    for W in [int(x) for x in (sys.argv[1:] or ["1", "2", "4", "8"])]:
+    jobs = [(int(x), 1) for x in (sys.argv[1:] or ["1", "2", "4", "8"])]
+    if hybrid:  # 2 replicas x W/2 shards: each rank half the batch on a 2/W shard
+        jobs += [(W // 2, 2) for W, _ in list(jobs) if W >= 4]
+    for Ws, R in jobs:  # Ws doc shards, R replicas (each replica takes Q/R queries)
+        W = Ws
+        q = q_full[:q_full.shape[0] // R].contiguous()
+        Q = q.shape[0]
         bounds = [synth.shard_bounds(cfg.n_docs, W, r) for r in range(W)]
         smax = max(hi - lo for lo, hi in bounds)
         shards = []
@@ -67,58 +148,91 @@ def main():
         S = shards[0].sample_width(k, W, smax)
         out_d = torch.empty((Q, k), dtype=torch.int32, device="cuda")
         out_s = torch.empty((Q, k), dtype=torch.float32, device="cuda")
-        if W == 1:
-            def one(r):
-                shards[0].search_device(q, k, out_d, out_s, st)
-        else:
-            keys = torch.empty((W, Q, S), dtype=torch.int64, device="cuda")
-            for r, ix_ in enumerate(shards):
-                ix_.search_sample_device(q, k, W, smax, keys[r], st)
-            g = torch.empty((W, 2, Q, k), dtype=torch.int32, device="cuda")
-            for r, ix_ in enumerate(shards):
-                ix_.search_finish_device(q, k, W, smax, keys, g[r, 0], g[r, 1].view(torch.float32), st)
-            torch.cuda.synchronize()
-
-            def one(r):
-                ix_ = shards[r]
-                ix_.search_sample_device(q, k, W, smax, keys[r], st)
-                ix_.search_finish_device(q, k, W, smax, keys, g[r, 0], g[r, 1].view(torch.float32), st)
-                merge_sorted_device(dev, g, g[:, 1].view(torch.float32), W, Q, k, 2 * Q * k,
-                                    out_d, out_s, st)
-        ranks = range(W) if not ranks_env else [int(x) for x in ranks_env.split(",") if int(x) < W]
-        per_rank = []
-        for r in ranks:
-            for _ in range(3):
-                one(r)
-            torch.cuda.synchronize()
-            shards[r].profile_enable(True)
-            t0 = time.perf_counter()
-            for _ in range(n):
-                one(r)
-            torch.cuda.synchronize()
-            ms = (time.perf_counter() - t0) * 1e3 / n
-            p = shards[r].profile_read()
-            shards[r].profile_enable(False)
-            per_rank.append({"rank": r, "ms": round(ms, 4),
-                             "score_ms": round(p["score_ms"] / max(p["score_launches"], 1), 4),
-                             "fallback_queries": shards[r].search_stats()["fallback_queries"]})
-        worst = max(x["ms"] for x in per_rank)
         keys_b = Q * S * 8
         list_b = Q * k * 8
-        coll_us = model_gather_us(keys_b, W) + model_gather_us(list_b, W)
-        proj = worst + coll_us * 1e-3
-        if W == 1:
-            w1_ms = worst
-        line = {"W": W, "shard_docs_max": smax, "sample_width": S, "per_rank": per_rank,
-                "max_rank_ms": round(worst, 4),
-                "model": {"alpha_us": ALPHA_US, "link_GBps": LINK_GBS,
-                          "keys_bytes_per_rank": keys_b, "list_bytes_per_rank": list_b,
-                          "collectives_us": round(coll_us, 1)},
-                "projected_ms": round(proj, 4),
-                "projected_qps": round(Q / proj * 1e3, 1)}
-        if w1_ms is not None:
-            line["speedup_vs_W1"] = round(w1_ms / proj, 3)
-        print(json.dumps(line), flush=True)
+        for P in parts_list:
+            for gp in grids:
+                for s_ in shards:
+                    s_.set_option("grid_pct", gp)
+                cuts = [Q * i // P for i in range(P + 1)]
+                rows = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+                inline = P > 1 or os.environ.get("PROBE_INLINE") == "1"
+                if W == 1 and P == 1:
+                    def one(r):
+                        shards[0].search_device(q, k, out_d, out_s, st)
+                else:
+                    # every shard's real sample keys and lists, per part
+                    keys_p, g_p = [], []
+                    for a, b in rows:
+                        kk = torch.zeros((W, b - a, max(S, 1)), dtype=torch.int64, device="cuda")
+                        for r, ix_ in enumerate(shards):
+                            if S > 0:
+                                ix_.search_sample_device(q[a:b], k, W, smax, kk[r], st)
+                        g = torch.empty((W, 2, b - a, k), dtype=torch.int32, device="cuda")
+                        for r, ix_ in enumerate(shards):
+                            ix_.search_finish_device(q[a:b], k, W, smax, kk, g[r, 0],
+                                                     g[r, 1].view(torch.float32), st)
+                        keys_p.append(kk)
+                        g_p.append(g)
+                    torch.cuda.synchronize()
+                    if inline:
+                        forks = {}
+                        streams = [torch.cuda.Stream() for _ in rows]
+                        comm = torch.cuda.Stream()
+                        kus = model_gather_us(keys_b // len(rows), W)
+                        lus = model_gather_us(list_b // len(rows), W)
+
+                        def one(r):
+                            if r not in forks:
+                                forks[r] = [shards[r].fork() for _ in rows[1:]]
+                            rank_parts(shards, r, q, k, W, smax, keys_p, g_p, rows, out_d,
+                                       out_s, forks[r], streams, comm, kus, lus)
+                    else:
+                        def one(r):
+                            ix_ = shards[r]
+                            ix_.search_sample_device(q, k, W, smax, keys_p[0][r], st)
+                            ix_.search_finish_device(q, k, W, smax, keys_p[0], g_p[0][r, 0],
+                                                     g_p[0][r, 1].view(torch.float32), st)
+                            merge_sorted_device(q.device.index, g_p[0],
+                                                g_p[0][:, 1].view(torch.float32), W, Q, k,
+                                                2 * Q * k, out_d, out_s, st)
+                ranks = (range(W) if not ranks_env else
+                         [int(x) for x in ranks_env.split(",") if int(x) < W])
+                per_rank = []
+                for r in ranks:
+                    for _ in range(3):
+                        one(r)
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for _ in range(n):
+                        one(r)
+                    torch.cuda.synchronize()
+                    ms = (time.perf_counter() - t0) * 1e3 / n
+                    per_rank.append({"rank": r, "ms": round(ms, 4),
+                                     "fallback_queries": shards[r].search_stats()["fallback_queries"]})
+                worst = max(x["ms"] for x in per_rank)
+                coll_us = 0.0 if inline else (model_gather_us(keys_b, W) + model_gather_us(list_b, W))
+                proj = worst + coll_us * 1e-3
+                if W == 1 and P == 1 and R == 1 and gp == 100:
+                    w1_ms = worst
+                line = {"W": W * R, "shards": W, "replicas": R, "parts": P, "grid_pct": gp,
+                        "queries_per_rank": Q, "shard_docs_max": smax, "sample_width": S,
+                        "per_rank": per_rank, "max_rank_ms": round(worst, 4),
+                        "model": {"alpha_us": ALPHA_US, "link_GBps": LINK_GBS,
+                                  "keys_bytes_per_rank": keys_b, "list_bytes_per_rank": list_b,
+                                  "collectives": ("inline spin kernels on one comm stream "
+                                                  "(measured with the step)" if inline else
+                                                  "added after the step (no overlap)"),
+                                  "collectives_us": round(coll_us if not inline else
+                                                          model_gather_us(keys_b // len(rows), W)
+                                                          * len(rows) +
+                                                          model_gather_us(list_b // len(rows), W)
+                                                          * len(rows), 1)},
+                        "projected_ms": round(proj, 4),
+                        "projected_qps": round(Q * R / proj * 1e3, 1)}
+                if w1_ms is not None:
+                    line["speedup_vs_W1"] = round(w1_ms / proj * R * Q / (Q * R), 3)
+                print(json.dumps(line), flush=True)
         for s_ in shards:
             s_.close()
         del shards

@@ -46,3 +46,13 @@ def test_algorithmic_bytes_formula():
     k = 10
     want = ((8 * 2 + 8) + (8 * 5 + 8) + 4 * 4 + 8 * k) + ((8 * 1 + 8) + 4 * 4 + 8 * k)
     assert bench.algorithmic_bytes(indptr, q, k) == want
+
+
+def test_posting_counts_per_query_and_batch_distinct():
+    # terms 0..3 with df 2, 0, 5, 1; query 0 = {0, 2} (2 repeated), query 1 = {3},
+    # query 2 = {2, 3}: per query 7 + 1 + 6, batch-distinct {0, 2, 3} = 8
+    indptr = np.array([0, 2, 2, 7, 8], np.int64)
+    q = np.array([[0, 2, 2, -1], [3, -1, -1, -1], [2, 3, -5, -1]], np.int32)
+    assert bench.query_postings(indptr, q) == 14
+    assert bench.batch_distinct_postings(indptr, q) == 8
+    assert bench.batch_distinct_postings(indptr, np.full((2, 3), -1, np.int32)) == 0

@@ -266,3 +266,121 @@ def test_gloo_sharded_search_checks(tmp_path):
     assert got["k_err"] == "kth(=-1) out of bounds (2001)"
     assert got["sub_docs"] == 1000 and got["world_docs"] == 2001
     assert "disagree on the sample width" in got["width_err"]
+
+
+class _NumpyShard:
+    """A doc shard that answers the two halves of the global-threshold
+    protocol on the host (numpy), with GpuIndex's call signatures: every
+    tile's best key as the sample (GLOBAL doc ids, zero-padded to the common
+    width), theta = the world sample's k-th key, the shard's keys >= theta
+    best first, padded with doc -1 / score bits ~0 as the HIP finish half
+    writes them.  fork() shares the data, as bm25_index_fork shares the
+    device arrays."""
+
+    def __init__(self, ip, ix, dt, lo, hi, tile, width):
+        self.ip, self.ix, self.dt, self.lo, self.hi = ip, ix, dt, lo, hi
+        self.n_docs, self.tile, self.width = hi - lo, tile, width
+        self.calls = []
+
+    def fork(self):
+        f = _NumpyShard(self.ip, self.ix, self.dt, self.lo, self.hi, self.tile, self.width)
+        f.calls = self.calls
+        return f
+
+    def sample_width(self, k, world, shard_docs_max):
+        return self.width
+
+    def _dense(self, row):
+        s = np.zeros(self.hi - self.lo, np.float32)
+        for t in row:
+            if t < 0:
+                continue
+            a, b = int(self.ip[t]), int(self.ip[t + 1])
+            sel = (self.ix[a:b] >= self.lo) & (self.ix[a:b] < self.hi)
+            np.add.at(s, self.ix[a:b][sel] - self.lo, self.dt[a:b][sel])
+        return s
+
+    def search_sample_device(self, q, k, world, sdm, keys, stream=None):
+        self.calls.append(("sample", q.shape[0]))
+        out = np.zeros(keys.shape, np.uint64)
+        for i, row in enumerate(q.numpy()):
+            s = self._dense(row)
+            for j in range(0, s.size, self.tile):
+                seg = s[j:j + self.tile]
+                m = int(np.argmax(seg))
+                out[i, j // self.tile] = _key(seg[m], self.lo + j + m) if seg[m] > 0 else 0
+        keys.copy_(torch.from_numpy(out.view(np.int64)))
+
+    def search_finish_device(self, q, k, world, sdm, all_keys, d_docs, d_scores, stream=None):
+        self.calls.append(("finish", q.shape[0]))
+        ak = all_keys.numpy().view(np.uint64)
+        docs = np.full((q.shape[0], k), -1, np.int32)
+        scores = np.full((q.shape[0], k), -1, np.int32).view(np.float32)  # bits ~0
+        for i, row in enumerate(q.numpy()):
+            theta = int(np.sort(ak[:, i, :].ravel())[::-1][k - 1])
+            s = self._dense(row)
+            u = s.view(np.uint32).astype(np.uint64)
+            sk = np.where(u & 0x80000000, ~u & 0xFFFFFFFF, u | 0x80000000)
+            docs_g = np.arange(self.lo, self.hi, dtype=np.uint64)
+            keys_ = (sk << np.uint64(32)) | (np.uint64(0xFFFFFFFF) - docs_g)
+            sel = np.nonzero(keys_ >= np.uint64(theta))[0]
+            lst = sorted(((int(keys_[d]), self.lo + int(d), s[d]) for d in sel), reverse=True)[:k]
+            for j, (_, d, v) in enumerate(lst):
+                docs[i, j], scores[i, j] = d, v
+        d_docs.copy_(torch.from_numpy(docs))
+        d_scores.copy_(torch.from_numpy(scores))
+
+
+def _merge_packed_cpu(device, g, g_scores, W, Q, k, stride, out_d, out_s, stream=None):
+    """bm25_merge_sorted_device on the host: [W][docs|scores][Q][k] -> [Q, k]."""
+    d = g[:, 0].contiguous()
+    s = g[:, 1].contiguous().view(torch.float32)
+    s = torch.where(d < 0, torch.full_like(s, -np.inf), s)  # padding sorts last
+    md, ms = _merge_cpu(d, s)
+    out_d.copy_(md)
+    out_s.copy_(ms)
+
+
+def _parts_worker(rank, world, port, args, k, tile, parts, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bm25mi.index as bi
+        from bm25mi.dist import shard_bounds, sharded_search
+        bi.merge_sorted_device = _merge_packed_cpu  # the host stand-in of the HIP merge
+        N, V, Q, T, seed = args
+        ip, ix, dt, q = _tie_index(N, V, Q, T, seed)
+        lo, hi = shard_bounds(N, world, rank, align=tile)
+        sdm = max(b - a for a, b in (shard_bounds(N, world, r, align=tile) for r in range(world)))
+        shard = _NumpyShard(ip, ix, dt, lo, hi, tile, (sdm + tile - 1) // tile)
+        d = torch.zeros((Q, k), dtype=torch.int32)
+        s = torch.zeros((Q, k), dtype=torch.float32)
+        sharded_search(shard, torch.from_numpy(q), k, sdm, d, s, parts=parts, n_docs_total=N)
+        if rank == 0:
+            np.savez(result_path, docs=d.numpy(), scores=s.numpy(),
+                     calls=np.array([c[1] for c in shard.calls]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,parts", [(2, 2), (3, 3)])
+def test_gloo_search_parts_protocol(tmp_path, world, parts):
+    """sharded_search(parts=P): the batch's rows as P parts on forks of the
+    shard, each through both halves and both all-gathers, merged into its own
+    rows — the single-index top-k bit for bit (tie-heavy index, tie groups
+    across shards), every part's sample and finish issued once."""
+    from oracle import oracle
+    args = (12000, 6, 7, 3, 11)
+    k, tile = 40, 256
+    out = str(tmp_path / "r.npz")
+    mp.spawn(_parts_worker, args=(world, _free_port(), args, k, tile, parts, out),
+             nprocs=world, join=True)
+    got = np.load(out)
+    ip, ix, dt, q = _tie_index(*args)
+    ref = oracle.search_c(args[0], ip, ix, dt, q, k)
+    assert np.array_equal(got["docs"], ref[0])
+    assert np.array_equal(got["scores"].view(np.uint32), ref[1].view(np.uint32))
+    cuts = [args[2] * i // parts for i in range(parts + 1)]
+    sizes = [b - a for a, b in zip(cuts[:-1], cuts[1:])]
+    assert list(got["calls"]) == sizes + sizes  # every sample half, then every finish half

@@ -31,7 +31,7 @@ CASES = {
 }
 
 
-def _worker(rank, world, port, case, out):
+def _worker(rank, world, port, case, out, parts=1):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -54,7 +54,10 @@ def _worker(rank, world, port, case, out):
         d_scores = torch.empty((len(q), cfg.k), dtype=torch.float32, device="cuda")
         stream = torch.cuda.Stream()   # a non-current stream: the body must order on it
         merge = gpu_merge(0, stream) if os.environ.get("BM25_TEST_MERGE") == "sort" else None
-        docs, scores = sharded_search(index, dq, cfg.k, sdm, d_docs, d_scores, merge, stream)
+        docs, scores = sharded_search(index, dq, cfg.k, sdm, d_docs, d_scores, merge, stream,
+                                      parts=parts)
+        if parts > 1:  # the parts ran on forks of the index, each on its own stream
+            assert len(index.__dict__["_bm25_forks"]) == parts - 1
         torch.cuda.synchronize()
         if rank == 0:
             np.savez(out, docs=docs.cpu().numpy(), scores=scores.cpu().numpy())
@@ -66,11 +69,23 @@ def _worker(rank, world, port, case, out):
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("case", ["synth", "small"])
 def test_sharded_search_real_process_group(gpu, tmp_path, world, case):
+    _run_case(tmp_path, world, case, 1)
+
+
+@pytest.mark.parametrize("world,case,parts", [(2, "synth", 2), (3, "small", 3), (2, "synth", 4)])
+def test_sharded_search_parts_real_process_group(gpu, tmp_path, world, case, parts):
+    """sharded_search(parts=P): the batch pipelined as P row ranges over forks
+    of each rank's shard (bm25_index_fork), each part on its own stream with
+    its own all-gathers — bit-exact like the unsplit search."""
+    _run_case(tmp_path, world, case, parts)
+
+
+def _run_case(tmp_path, world, case, parts):
     from bm25mi import synth
     from oracle import oracle
     cfg = synth.Config(*CASES[case])
     out = str(tmp_path / "r.npz")
-    mp.spawn(_worker, args=(world, _free_port(), case, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), case, out, parts), nprocs=world, join=True)
     got = np.load(out)
     q = synth.make_queries(cfg)
     q[2, 3:] = -1

@@ -698,6 +698,35 @@ def test_global_theta_sharded_search(gpu, W):
     _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)
 
 
+def test_split_halves_all_padding_row_k1(gpu):
+    """The two halves of the sharded protocol on a 2-tile index with an
+    all-padding row at k = 1 (the case round 4's debug probes chased): the
+    row's top-1 is doc 0 at score 0 whether the world's sample holds this
+    shard's own keys or only zeros (a world whose other shards hold nothing),
+    and the other row is the oracle's."""
+    import torch
+    rng = np.random.default_rng(1)
+    N, V = 3000, 20
+    ip, ix, dt = _rand_index(rng, N, V, N // 3)
+    index = _idx(ip, ix, dt, N)
+    q = np.array([[-1, -1, -1], [1, 2, -1]], np.int32)
+    dq = torch.from_numpy(q).cuda()
+    for k in (1, 3):
+        ref = oracle.search_c(N, ip, ix, dt, q, k)
+        S = index.sample_width(k, 1, N)
+        for world_keys in ("own", "zeros"):
+            keys = torch.full((2, max(S, 1)), 7, dtype=torch.int64, device="cuda")
+            if S > 0:
+                index.search_sample_device(dq, k, 1, N, keys)
+            ak = keys if world_keys == "own" else torch.zeros_like(keys)
+            d = torch.empty((2, k), dtype=torch.int32, device="cuda")
+            s = torch.empty((2, k), dtype=torch.float32, device="cuda")
+            index.search_finish_device(dq, k, 1, N, ak.unsqueeze(0), d, s)
+            torch.cuda.synchronize()
+            _exact((d.cpu().numpy(), s.cpu().numpy()), ref)
+    index.close()
+
+
 def _doc_slice(indptr, indices, data, lo, hi):
     """The CSC of documents [lo, hi) (local ids), columns kept."""
     ip = np.zeros(len(indptr), np.int64)
@@ -1076,11 +1105,17 @@ def test_tile_bound_skips_exact(gpu, T):
     for k in (10, 100):
         ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
         _exact(index.search(q, k), ref)
-        skipped = index.search_stats()["bound_skipped_tiles"]
+        st = index.search_stats()
+        skipped = st["bound_skipped_tiles"]
         assert skipped > 0, skipped
+        # the postings of the skipped pairs (bench.py's roofline.bound_skip)
+        df = np.diff(ip)
+        per_query = sum(int(df[np.unique(r[r >= 0])].sum()) for r in q)
+        assert 0 < st["bound_skipped_postings"] < per_query, (st, per_query)
         index.set_option("tile_bound", 0)
         _exact(index.search(q, k), ref)
-        assert index.search_stats()["bound_skipped_tiles"] == 0
+        st = index.search_stats()
+        assert st["bound_skipped_tiles"] == 0 and st["bound_skipped_postings"] == 0
         index.set_option("tile_bound", 1)
 
 
@@ -1182,3 +1217,34 @@ def test_theta_bound_sharded_protocol(gpu):
         _exact((od.cpu().numpy(), os_.cpu().numpy()), ref)
     for s in shards:
         s.close()
+
+
+def test_fork_shares_arrays_concurrent_streams(gpu):
+    """bm25_index_fork: a second context on the same device arrays with its
+    own workspace — two halves of a batch searched at once on two streams
+    (one per handle) give the oracle's bits; options are copied at fork time
+    and follow set_option; the fork outlives its base (shared arrays)."""
+    import torch
+    from bm25mi import synth
+    cfg = synth.Config("f", 700_000, 3000, 5_000_000, 96, 8, 50)
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k)
+    base = _idx(ip, ix, dt, cfg.n_docs, options={"grid_pct": 60})
+    fork = base.fork()
+    assert fork.get_option("grid_pct") == 60 and fork.info() == base.info()
+    dq = torch.from_numpy(q).cuda()
+    d = torch.empty((len(q), cfg.k), dtype=torch.int32, device="cuda")
+    s = torch.empty((len(q), cfg.k), dtype=torch.float32, device="cuda")
+    h = len(q) // 2
+    s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        base.search_device(dq[:h], cfg.k, d[:h], s[:h], s0)
+        fork.search_device(dq[h:], cfg.k, d[h:], s[h:], s1)
+    torch.cuda.synchronize()
+    _exact((d.cpu().numpy(), s.cpu().numpy()), ref)
+    with pytest.raises(ValueError, match="grid_pct"):
+        base.set_option("grid_pct", 0)
+    base.close()  # the fork keeps the arrays
+    _exact(fork.search(q, cfg.k), ref)
+    fork.close()
