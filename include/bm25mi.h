@@ -354,7 +354,11 @@ int bm25_index_get_option(const bm25_index* idx, const char* name, int64_t* valu
  *   *kernels     bit mask of score kernels: 1 flat SAMPLE, 2 flat REST,
  *                4 flat ALL (exact pass / fallback stage), 8 wave SAMPLE,
  *                16 wave REST, 32 wave ALL, 64 large-k path, 128 tile-bound
- *                threshold keys
+ *                threshold keys; 256 (a flag, not a kernel): the tile-bound
+ *                threshold was off for this search because earlier searches
+ *                on the handle that used it overflowed their candidate lists
+ *                (more than 1/16 of their queries took the exact fallback) —
+ *                it is retried after 64, 128, ... 4096 searches
  *   *term_lanes  flat kernel: term lanes per tile (8, 16, 32 or 64)
  *   band_tiles   [3]: flat kernel tiles per item of ALL, SAMPLE, REST
  *   *sample_p    sampling stride of the search (1: exact pass, 0: tile-bound

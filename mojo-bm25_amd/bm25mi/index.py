@@ -221,7 +221,8 @@ class GpuIndex:
         return v.value
 
     KERNELS = {1: "flat_sample", 2: "flat_rest", 4: "flat_all", 8: "wave_sample",
-               16: "wave_rest", 32: "wave_all", 64: "large_k", 128: "bound_keys"}
+               16: "wave_rest", 32: "wave_all", 64: "large_k", 128: "bound_keys",
+               256: "bound_off"}  # (256: a flag — the tile-bound threshold was off)
 
     def last_dispatch(self) -> dict:
         """What the last search launched (bm25_search_dispatch): the score

@@ -91,6 +91,12 @@ struct bm25_index {
   hipStream_t ws_stream = nullptr; // its stream
   int32_t* d_maxtok = nullptr;     // bm25_max_token_device result
   bool sampled = false;            // a sample half ran since the last finish half
+  // the threshold source (choose_theta_source): host-mapped report of the
+  // searches' overflow, the search sequence, the last tile-bound search
+  int32_t* report_host = nullptr;
+  int32_t* report_dev = nullptr;
+  int32_t seq = 0, last_bound_seq = -1, seen_seq = -1, weak_until = 0, backoff = 64;
+  int64_t last_bound_q = 0;
 };
 
 namespace {
@@ -299,6 +305,62 @@ hipError_t order_ws(bm25_index* h, hipStream_t st) {
   return hipStreamWaitEvent(st, h->ws_done, 0);
 }
 
+// The threshold source of the handle's next search (DevIndex::bound_weak).
+// A search that took the tile-bound threshold and sent more than 1/16 of its
+// queries to the exact fallback stage — their candidate lists overflowed:
+// the single-term tile maxima sit far below the best sums, as on an index
+// whose terms all weigh alike — turns that threshold off for the next
+// `backoff` searches (64, doubling while it keeps failing, at most 4096),
+// which take the sampled threshold instead.  The overflow comes from the
+// host-mapped report merge_tail_kernel writes at the end of a search: no
+// wait — a report not written yet leaves the choice as it is.  Every choice
+// is exact; only the cost differs.  Caller holds h->mu.
+void choose_theta_source(bm25_index* h) {
+  ++h->seq;
+  if (h->report_host && h->last_bound_seq >= 0 && h->seen_seq != h->last_bound_seq) {
+    const int32_t r = __atomic_load_n(h->report_host + 1, __ATOMIC_ACQUIRE);
+    if (r == h->last_bound_seq) {
+      h->seen_seq = r;
+      const int64_t nf = __atomic_load_n(h->report_host, __ATOMIC_RELAXED);
+      if (nf * 16 > h->last_bound_q) {
+        h->weak_until = h->seq + h->backoff;
+        h->backoff = std::min(2 * h->backoff, 4096);
+      } else {
+        h->backoff = 64;
+      }
+    }
+  }
+  h->ix.bound_weak = h->seq < h->weak_until;
+}
+
+// The search's report slot and sequence number in the workspace (after
+// ensure_ws, which may rebuild it); P = 0: it took the tile-bound threshold.
+void arm_report(bm25_index* h, int P, int64_t Q) {
+  h->ws.report = h->report_dev;
+  h->ws.seq = h->seq;
+  if (h->ix.bound_weak) h->ix.disp.kernels |= kKBoundOff;
+  if (P == 0) {
+    h->last_bound_seq = h->seq;
+    h->last_bound_q = Q;
+  }
+}
+
+void alloc_report(bm25_index* h) {
+  if (hipHostMalloc((void**)&h->report_host, 2 * sizeof(int32_t), hipHostMallocMapped) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    h->report_host = nullptr;
+    return;
+  }
+  h->report_host[0] = 0;
+  h->report_host[1] = -1;
+  if (hipHostGetDevicePointer((void**)&h->report_dev, h->report_host, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    hipHostFree(h->report_host);
+    h->report_host = h->report_dev = nullptr;
+  }
+}
+
 // Device pipeline on stream st; caller holds h->mu and has set the device.
 int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, int k,
                int32_t* d_docs, float* d_scores, hipStream_t st) {
@@ -329,9 +391,11 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   int rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
+  choose_theta_source(h);
   const int P = search_geom(h->ix, h->ix.ntiles, k, 1, T).P;
   h->ix.disp = Dispatch{};
   h->ix.disp.sample_p = P;
+  arm_report(h, P, Q);
   EventPair* ev = next_events(h);
   if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
   HIP_TRY(launch_score(h->ix, d_queries, Q, T, k, h->ws, st), "score launch");
@@ -442,6 +506,7 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     if (e != hipSuccess) return cleanup(hip_fail(e, what));       \
   } while (0)
   TRYC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+  alloc_report(h);
   // segment table form (DevIndex): BM25_SEGMENTS=dense|sparse; by default the
   // dense V x (ntiles+1) table (O(1) lookups, no per-search table: config 5's
   // 24 GB per rank ran 6 % faster than the tile lists) unless it would
@@ -549,6 +614,7 @@ int bm25_index_destroy(bm25_index* h) {
   hipFree(h->d_docs);
   hipFree(h->d_scores);
   hipFree(h->d_maxtok);
+  if (h->report_host) hipHostFree(h->report_host);
   if (h->arrays) {
     h->arrays.reset();  // the index arrays go with the last handle sharing them
   } else {              // a create that failed part-way
@@ -578,6 +644,7 @@ int bm25_index_fork(bm25_index* base, bm25_index** out) {
     bm25_index_destroy(h);
     return hip_fail(e, "hipStreamCreate");
   }
+  alloc_report(h);
   *out = h;
   return BM25_OK;
 }
@@ -701,9 +768,11 @@ int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   HIP_TRY(order_ws(h, st), "workspace order");
   h->split_ev = next_events(h);
   if (h->split_ev) HIP_TRY(hipEventRecord(h->split_ev->a, st), "hipEventRecord");
+  choose_theta_source(h);  // (the finish half keeps this choice)
   const SampleGeom g = shard_geom(h, shard_docs_max, world, k, T);
   h->ix.disp = Dispatch{};
   h->ix.disp.sample_p = g.P;
+  arm_report(h, g.P, Q);
   h->sampled = true;
   HIP_TRY(launch_sample(h->ix, d_queries, Q, T, g, d_keys, h->ws, st), "sample launch");
   return BM25_OK;
@@ -728,10 +797,15 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   rc = ensure_ws(h, Q, T, k);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
+  if (!h->sampled) choose_theta_source(h);  // no sample half ran for this search (S = 0)
   const SampleGeom g = shard_geom(h, shard_docs_max, world, k, T);
-  if (!h->sampled) {  // no sample half ran for this search (S = 0)
+  if (!h->sampled) {
     h->ix.disp = Dispatch{};
     h->ix.disp.sample_p = g.P;
+    arm_report(h, g.P, Q);
+  } else {
+    h->ws.report = h->report_dev;  // (ensure_ws may have rebuilt the workspace)
+    h->ws.seq = h->seq;
   }
   h->sampled = false;
   HIP_TRY(launch_finish(h->ix, d_queries, Q, T, k, g, world, d_all_keys, h->ws, st),

@@ -84,6 +84,8 @@ enum {
   kKWaveSample = 8, kKWaveRest = 16, kKWaveAll = 32,
   kKLarge = 64,  // the large-k path (k > kMaxK): dense scores + radix selection
   kKBound = 128, // tile-bound threshold keys (bound_keys_kernel) instead of a SAMPLE pass
+  kKBoundOff = 256,  // (not a kernel) the tile-bound threshold was off for this search:
+                     // earlier ones overflowed with it (DevIndex::bound_weak)
 };
 struct Dispatch {
   uint32_t kernels = 0;       // kK* bits of the score kernels launched
@@ -121,6 +123,11 @@ struct DevIndex {
   // bound of that score (threshold keys) and, one f16 step up, an upper bound
   // (the REST pass's tile skip)
   uint16_t* bmax = nullptr;
+  // The tile-bound threshold is off for this handle's next searches: the
+  // last ones that used it overflowed their candidate lists (weak bounds —
+  // an index whose terms weigh alike); set by the host per search
+  // (bm25mi_capi.cpp: bound_ok), read by search_geom
+  bool bound_weak = false;
   SearchOpts opt;
   mutable Dispatch disp;  // written by the launchers (callers hold the handle's mutex)
 };
@@ -149,6 +156,9 @@ struct Workspace {
                                  // at allocation; the last wave of each counter's sharers
                                  // re-zeroes it (and its finished count) at the end of every
                                  // flat launch, so each launch finds its region zeroed
+  int32_t* report = nullptr;     // host-mapped [2]: merge_tail_kernel writes the search's
+                                 // fallback query count, then `seq` (null: no report)
+  int32_t seq = 0;               // the search's sequence number on its handle
   uint64_t* seg = nullptr;       // sparse index: [Q][tiles/8][TT][8] segment of each (query,
                                  // term position, tile) (start | len << 32), built per search
   int64_t cap_seg = 0;           // u64 entries of seg

@@ -2521,6 +2521,12 @@ __global__ __launch_bounds__(kMergeNT) void merge_tail_kernel(
   __shared__ int32_t s_nflag, s_cnt;
   __shared__ uint32_t zf_bits[2 * kMaxK / 32];
   static_assert((1 << S) <= kMergeP, "rescore keys live in the merge buffer");
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ws.report != nullptr) {
+    // the search's overflow, for the host's choice of the next threshold
+    // source (bound_ok): the count, then the sequence number that marks it valid
+    __hip_atomic_store(ws.report, (int32_t)stage_nq(fb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.report + 1, ws.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const int64_t ns = stage_nq(sl);
   for (int64_t i = blockIdx.x; i < ns; i += gridDim.x) {
     __syncthreads();
@@ -2731,7 +2737,8 @@ SampleGeom sample_geom(int64_t ntiles, int k, int W, int pmax) {
 SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W, int64_t T) {
   const SampleGeom g = sample_geom(ntiles, k, W, ix.opt.sample_p);
   const bool bounds = ix.ntiles == 0 || (ix.bmax != nullptr && ix.nonneg && !ix.sparse);
-  if (g.P > 1 && ix.opt.theta_bound && bounds && k >= 1 && T >= 1 && T <= kBoundMaxTerms &&
+  if (g.P > 1 && ix.opt.theta_bound && !ix.bound_weak && bounds && k >= 1 && T >= 1 &&
+      T <= kBoundMaxTerms &&
       ntiles <= kBoundMaxTiles && ntiles * std::max(W, 1) >= kBoundTilesPerK * (int64_t)k)
     return SampleGeom{0, 1, g.S, 1};
   return g;

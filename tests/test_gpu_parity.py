@@ -207,8 +207,7 @@ def test_flat_kernel_query_widths(gpu, T, lanes, segments):
     for k in (1, 25, 300):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
         d = index.last_dispatch()
-        P = _geom_p(index, k, T=T)
-        assert d["kernels"] == _want_kernels(P) and d["sample_p"] == P, d
+        _check_dispatch(index, k, T=T)
         assert d["term_lanes"] == lanes, d
         assert 1 <= d["band_tiles"]["rest" if P != 1 else "all"] <= 64 // lanes
 
@@ -227,10 +226,10 @@ def test_wave_kernel_long_and_empty_queries(gpu, T):
     index = _idx(ip, ix, dt, N)
     for k in (1, 30, 200):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
-        assert index.last_dispatch()["kernels"] == _want_kernels(_geom_p(index, k, T=T), flat=False)
+        _check_dispatch(index, k, T=T, flat=False)
     index.set_option("sample_p", 1)  # the exact pass over every tile
     _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
-    assert index.last_dispatch()["kernels"] == {"wave_all"}
+    assert index.last_dispatch()["kernels"] - {"bound_off"} == {"wave_all"}
     index.set_option("list_cap", 4)  # every query through the fallback stage
     index.set_option("sample_p", 8)
     _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
@@ -270,7 +269,8 @@ def test_rescore_path_clustered_tile(gpu):
             got = index.search(q, k)
             _exact(got, oracle.search_c(N, ip, ix, dt, q, k))
             assert index.profile_read()["rescored_tiles_last"] > 0
-            assert index.last_dispatch()["kernels"] == {"flat_all" if flat else "wave_all"}
+            assert (index.last_dispatch()["kernels"] - {"bound_off"}
+                    == {"flat_all" if flat else "wave_all"})
 
 
 def test_search_device_torch(gpu):
@@ -427,20 +427,34 @@ def _sample_p(ntiles, k, W=1, pmax=8):
     return 1
 
 
-def _geom_p(index, k, W=1, ntiles=None, opts=None, T=8):
+def _geom_p(index, k, W=1, ntiles=None, opts=None, T=8, weak=False):
     """The threshold geometry search_geom picks (bm25mi_kernels.hip): 0 =
     tile-bound keys (a sampled geometry, the index keeps tile bounds,
     theta_bound on, queries of 1..16 terms, at most 30720 tiles, a collection
-    of >= 16k tiles), else _sample_p's stride."""
+    of >= 16k tiles, and not turned off for the handle after overflowing
+    searches — ``weak``, the dispatch's "bound_off" flag), else _sample_p's
+    stride."""
     opts = opts or {}
     info = index.info()
     nt = info["n_tiles"] if ntiles is None else ntiles
     pmax = opts.get("sample_p", 8)
     P = _sample_p(nt, k, W, pmax)
     if (P > 1 and opts.get("theta_bound", 1) and info["tile_bounds"] and 1 <= T <= 16
-            and nt <= 30720 and nt * W >= 16 * k):
+            and nt <= 30720 and nt * W >= 16 * k and not weak):
         return 0
     return P
+
+
+def _check_dispatch(index, k, W=1, ntiles=None, opts=None, T=8, flat=True):
+    """The last search launched the kernels of the geometry it should have
+    taken (with the tile-bound threshold off when the dispatch says the
+    handle turned it off after overflowing searches); returns the report."""
+    d = index.last_dispatch()
+    weak = "bound_off" in d["kernels"]
+    P = _geom_p(index, k, W, ntiles, opts, T=T, weak=weak)
+    want = _want_kernels(P, flat)
+    assert d["kernels"] - {"bound_off"} == want and d["sample_p"] == P, (k, d, want, P)
+    return d
 
 
 # (options, segment table)
@@ -472,7 +486,7 @@ def test_kernel_variants_bit_exact(gpu, opts, segments, T):
     q[4, 2:] = q[4, 1]
     index = _idx(ip, ix, dt, N, segments=segments)
     _exact(index.search(q, 7), oracle.search_c(N, ip, ix, dt, q, 7))  # defaults first
-    assert index.last_dispatch()["kernels"] == _want_kernels(_geom_p(index, 7, T=T))
+    _check_dispatch(index, 7, T=T)
     assert index.info()["tile_bounds"] == (segments == "dense")
     for name, val in opts.items():
         index.set_option(name, val)
@@ -482,10 +496,8 @@ def test_kernel_variants_bit_exact(gpu, opts, segments, T):
     fallback = 0
     for k in (1, 7, 100):
         _exact(index.search(q, k), oracle.search_c(N, ip, ix, dt, q, k))
-        d = index.last_dispatch()
-        P = _geom_p(index, k, 1, ntiles, opts, T=T)
-        want = _want_kernels(P, flat)
-        assert d["kernels"] == want and d["sample_p"] == P, (k, d, want, P)
+        d = _check_dispatch(index, k, 1, ntiles, opts, T=T, flat=flat)
+        P = d["sample_p"]
         if flat:
             assert d["term_lanes"] == (8 if T == 8 else 16)
             phase = "rest" if P != 1 else "all"
@@ -627,6 +639,47 @@ def test_merge_paths_long_lists(gpu):
     index.set_option("theta_bound", 1)
     _exact(index.search(q, 10), oracle.search_c(N, ip, ix, dt, q, 10))
     assert index.last_dispatch()["sample_p"] == 0
+
+
+def test_weak_bounds_switch_to_sampled_threshold(gpu):
+    """on an index whose terms all weigh alike, the
+    tile-bound threshold sits far below the best sums and the lists
+    overflow.  The first search with it sends its queries to the exact
+    fallback (still exact); the handle reads that overflow from the search's
+    report and its next 64 searches take the sampled threshold — exact, no
+    fallback — before the tile-bound one is retried (and, failing again, off
+    for 128)."""
+    rng = np.random.default_rng(33)
+    N, V = 6_000_000, 300
+    ip, ix, dt = _rand_index(rng, N, V, 400_000)
+    q = rng.integers(-1, V, size=(24, 8)).astype(np.int32)
+    ref = oracle.search_c(N, ip, ix, dt, q, 10)
+    index = _idx(ip, ix, dt, N)
+    _exact(index.search(q, 10), ref)
+    d = index.last_dispatch()
+    assert d["sample_p"] == 0 and "bound_off" not in d["kernels"], d
+    assert index.search_stats()["fallback_queries"] * 16 > len(q)
+    for i in range(64):
+        _exact(index.search(q, 10), ref)
+        d = _check_dispatch(index, 10)
+        assert "bound_off" in d["kernels"] and d["sample_p"] > 1, (i, d)
+        assert index.search_stats()["fallback_queries"] == 0
+    _exact(index.search(q, 10), ref)  # the retry
+    assert index.last_dispatch()["sample_p"] == 0
+    for i in range(128):
+        _exact(index.search(q, 10), ref) if i % 32 == 0 else index.search(q, 10)
+        assert "bound_off" in index.last_dispatch()["kernels"], i
+    # a skewed index keeps the tile-bound threshold
+    from bm25mi import synth
+    cfg = synth.Config("s", 2_000_000, 20_000, 12_000_000, 40, 8, 10)
+    ip2, ix2, dt2 = synth.make_index(cfg)
+    q2 = synth.make_queries(cfg)
+    index2 = _idx(ip2, ix2, dt2, cfg.n_docs)
+    ref2 = oracle.search_c(cfg.n_docs, ip2, ix2, dt2, q2, cfg.k)
+    for _ in range(4):
+        _exact(index2.search(q2, cfg.k), ref2)
+        d = index2.last_dispatch()
+        assert d["sample_p"] == 0 and "bound_off" not in d["kernels"], d
 
 
 def test_rare_queries_zero_fill_path(gpu):
@@ -1025,7 +1078,8 @@ def test_config4_c3_index_eight_shards_full_batch(gpu):
         _progress(f"c4: rank shard [{lo}, {hi}) built")
     _exact(_protocol_search(shards, torch.from_numpy(q).cuda(), cfg.k, sdm), ref)
     d = shards[0].last_dispatch()
-    assert d["kernels"] == _want_kernels(_geom_p(shards[0], cfg.k, W, (sdm + 2047) // 2048)), d
+    assert d["kernels"] - {"bound_off"} == _want_kernels(
+        _geom_p(shards[0], cfg.k, W, (sdm + 2047) // 2048, weak="bound_off" in d["kernels"])), d
     for s in shards:
         s.close()
 
@@ -1050,7 +1104,7 @@ def test_config5_rank_shard_full_batch(gpu, segments):
     _progress(f"c5: {segments} index built")
     assert index.info()["sparse"] == (segments == "sparse")
     _exact(index.search(q, cfg.k), (rd + lo, rs))
-    assert index.last_dispatch()["kernels"] == _want_kernels(_geom_p(index, cfg.k))
+    _check_dispatch(index, cfg.k)
     assert index.info()["tile_bounds"] == (segments == "dense")
     assert index.search_stats()["fallback_queries"] == 0
     index.close()
@@ -1165,10 +1219,10 @@ def test_theta_bound_exact(gpu, T, big):
                 index.set_option("theta_bound", tb)
                 index.set_option("tile_bound", tl)
                 _exact(index.search(q, k), ref)
-                d = index.last_dispatch()
-                P = _geom_p(index, k, opts={"theta_bound": tb}, T=T)
-                assert (P == 0) == (bool(tb) and T <= 16), (P, tb, T)
-                assert d["kernels"] == _want_kernels(P, flat=T <= 64) and d["sample_p"] == P, d
+                d = _check_dispatch(index, k, opts={"theta_bound": tb}, T=T, flat=T <= 64)
+                P = d["sample_p"]
+                assert (P == 0) == (bool(tb) and T <= 16 and "bound_off" not in d["kernels"]), \
+                    (P, tb, T, d)
     index.set_option("theta_bound", 1)
     index.set_option("tile_bound", 1)
     index.close()
