@@ -169,7 +169,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", help="c3 (headline), c2, c5 (100M docs: one GPU "
-                    "runs one rank's doc shard, see --c5-rank)")
+                    "runs one rank's doc shard, see --c5-rank); side lines: c3u (config 3 with "
+                    "uniform weights: terms weigh alike), c3l (config 3's postings with "
+                    "lucene scores: tf saturation and document lengths, built on the GPU)")
     ap.add_argument("--c5-rank", type=int, default=0,
                     help="config 5 at N=1: which of the 8 doc shards of the 8-GPU job to run")
     ap.add_argument("--cpu-queries", type=int, default=64,
@@ -236,7 +238,13 @@ def main():
     else:
         lo, hi = synth.shard_bounds(cfg.n_docs, world, rank)
     t0 = time.time()
-    indptr, indices, data = synth.make_index(cfg, lo, hi, threads=args.threads)
+    if cfg.weights == "lucene" and args.cpu_queries > 0:
+        # its scores are built on the GPU (bm25_build_scores), and the CPU
+        # baseline's process pool must fork before this process touches it
+        log("note: --config c3l builds its scores on the GPU: no CPU baseline (--cpu-queries 0)")
+        args.cpu_queries = 0
+    local0 = local % max(torch.cuda.device_count(), 1)
+    indptr, indices, data = synth.make_index(cfg, lo, hi, threads=args.threads, device=local0)
     log(f"[rank {rank}] shard docs [{lo},{hi}) nnz={int(indptr[-1])} generated in "
         f"{time.time() - t0:.1f}s")
     queries = synth.make_queries(cfg)
@@ -383,7 +391,8 @@ def main():
             "native_lib": os.path.relpath(_capi.LIB, REPO),
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded Zipf CSC index + df^0.75 queries, csrc/synth.cpp)",
+            "data": "synthetic (seeded Zipf CSC index + df^0.75 queries, csrc/synth.cpp; "
+                    f"weights: {cfg.weights})",
             "config": {
                 "workload": f"{args.config}: {cfg.name}, {T} terms per query" + (
                     f"; one rank's doc shard [{lo}, {hi}) of the 8-GPU job" if emul else "") + (

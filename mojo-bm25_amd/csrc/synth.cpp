@@ -15,6 +15,13 @@
 //                ln(1 + (N - df + 0.5) / (df + 0.5)) of df_target
 //   queries      T distinct terms per query, drawn with probability
 //                proportional to df_target^beta (beta = 0.75)
+// Other weightings of the same postings (bm25_synth_fill_w, side lines of the
+// bench — VERDICT r4 item 4):
+//   uniform      0.05 + 2.95 * u for every term: terms weigh alike (the
+//                tile-bound threshold's worst case)
+//   tf           the term frequency 1 + Poisson(0.6) of each posting, for a
+//                lucene-scored index built by bm25_build_scores (bm25s's
+//                formula with tf saturation and document lengths)
 #include <stdint.h>
 
 #include <algorithm>
@@ -96,9 +103,26 @@ Plan make_plan(int64_t N, int64_t V, int64_t nnz, double alpha) {
   return p;
 }
 
+enum { kWeightIdf = 0, kWeightUniform = 1, kWeightTf = 2 };
+
+// 1 + Poisson(0.6) from 24 uniform bits (inversion)
+inline float poisson_tf(uint64_t x) {
+  double u = (double)((x >> 16) & 0xFFFFFF) * (1.0 / 16777216.0);
+  const double lam = 0.6;
+  double pk = std::exp(-lam), cdf = pk;
+  int k = 0;
+  while (u >= cdf && k < 30) {
+    ++k;
+    pk *= lam / k;
+    cdf += pk;
+  }
+  return (float)(1 + k);
+}
+
 // Walk the postings of term t inside [lo, hi); emit(doc, value).
 template <class F>
-void walk_term(const Plan& p, uint64_t seed, int64_t t, int64_t lo, int64_t hi, F&& emit) {
+void walk_term(const Plan& p, uint64_t seed, int64_t t, int64_t lo, int64_t hi, F&& emit,
+               int weights = kWeightIdf) {
   if (lo >= hi) return;
   const int64_t c0 = lo / kChunk, c1 = (hi + kChunk - 1) / kChunk;
   for (int64_t c = c0; c < c1; ++c) {
@@ -117,8 +141,13 @@ void walk_term(const Plan& p, uint64_t seed, int64_t t, int64_t lo, int64_t hi, 
       const uint64_t x = rng.next();
       const int64_t doc = base + pos;
       if (doc < lo || doc >= hi) continue;
-      const float u = 0.1f + 0.9f * ((float)(x >> 40) * (1.0f / 16777216.0f));
-      emit(doc, p.idf[t] * u);
+      const float r = (float)(x >> 40) * (1.0f / 16777216.0f);
+      if (weights == kWeightUniform)
+        emit(doc, 0.05f + 2.95f * r);
+      else if (weights == kWeightTf)
+        emit(doc, poisson_tf(x));
+      else
+        emit(doc, p.idf[t] * (0.1f + 0.9f * r));
     }
   }
 }
@@ -169,11 +198,13 @@ int bm25_synth_count(int64_t N, int64_t V, int64_t nnz, double alpha, uint64_t s
   return 0;
 }
 
-// indices are local to the shard (doc - doc_lo)
-int bm25_synth_fill(int64_t N, int64_t V, int64_t nnz, double alpha, uint64_t seed,
-                    int64_t doc_lo, int64_t doc_hi, int nthreads, const int64_t* indptr,
-                    int32_t* indices, float* data) {
+// indices are local to the shard (doc - doc_lo); weights: kWeight* (data =
+// the score, or the term frequency for kWeightTf)
+int bm25_synth_fill_w(int64_t N, int64_t V, int64_t nnz, double alpha, uint64_t seed,
+                      int64_t doc_lo, int64_t doc_hi, int nthreads, const int64_t* indptr,
+                      int32_t* indices, float* data, int weights) {
   if (N <= 0 || V < 0 || doc_lo < 0 || doc_hi > N || doc_lo > doc_hi || !indptr) return 1;
+  if (weights < kWeightIdf || weights > kWeightTf) return 1;
   const Plan p = make_plan(N, V, nnz, alpha);
   std::atomic<int> bad{0};
   parallel_terms(V, nthreads, [&](int64_t t) {
@@ -185,10 +216,17 @@ int bm25_synth_fill(int64_t N, int64_t V, int64_t nnz, double alpha, uint64_t se
         data[o] = v;
       }
       ++o;
-    });
+    }, weights);
     if (o != e) bad.store(1);
   });
   return bad.load();
+}
+
+int bm25_synth_fill(int64_t N, int64_t V, int64_t nnz, double alpha, uint64_t seed,
+                    int64_t doc_lo, int64_t doc_hi, int nthreads, const int64_t* indptr,
+                    int32_t* indices, float* data) {
+  return bm25_synth_fill_w(N, V, nnz, alpha, seed, doc_lo, doc_hi, nthreads, indptr, indices,
+                           data, kWeightIdf);
 }
 
 // queries[Q][T]: T distinct terms each, P(t) ~ df[t]^beta

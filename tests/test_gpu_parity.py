@@ -682,6 +682,26 @@ def test_weak_bounds_switch_to_sampled_threshold(gpu):
         assert d["sample_p"] == 0 and "bound_off" not in d["kernels"], d
 
 
+def test_lucene_synth_index_built_on_gpu(gpu):
+    """bench --config c3l's generator at a small scale: term frequencies and
+    document lengths scored on the GPU by bm25_build_scores (lucene rule) are
+    the oracle restatement's bits (oracle.build_scores_numpy, pinned by the
+    animal fixture), and a search of the result is the oracle's."""
+    from bm25mi import synth
+    cfg = synth.Config("l", 300_000, 3000, 2_000_000, 48, 8, 20, weights="lucene")
+    ip, ix, dt = synth.make_index(cfg)
+    _, _, tf = synth._fill(cfg, 0, None, 0, synth.WEIGHTS["tf"])
+    terms = np.repeat(np.arange(cfg.n_terms), np.diff(ip))
+    dl = np.bincount(ix, weights=tf, minlength=cfg.n_docs).astype(np.int32)
+    rip, rix, rdt, _ = oracle.build_scores_numpy(ix, terms, tf, dl, cfg.n_terms, 1.5, 0.75,
+                                                 "lucene", float(np.mean(dl.tolist())))
+    assert np.array_equal(rip, ip) and np.array_equal(rix, ix)
+    assert np.array_equal(rdt.view(np.uint32), dt.view(np.uint32))
+    q = synth.make_queries(cfg)
+    index = _idx(ip, ix, dt, cfg.n_docs)
+    _exact(index.search(q, cfg.k), oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k))
+
+
 def test_rare_queries_zero_fill_path(gpu):
     """Queries with fewer than k positive docs in the sample (rare terms) on a
     non-negative index: every positive doc + the smallest untouched ids —

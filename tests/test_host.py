@@ -172,3 +172,19 @@ def test_build_scores_validation_without_gpu():
         build_scores([0], [0], [1.0], [1], 1, method="okapi")
     with pytest.raises(ValueError, match="same length"):
         build_scores([0, 1], [0], [1.0], [1, 1], 1)
+
+
+def test_synth_weight_modes_share_postings():
+    """The side-line weightings (bench --config c3u / c3l) keep config 3's
+    postings: same indptr/indices, uniform values in [0.05, 3], term
+    frequencies 1 + Poisson(0.6) (mean 1.6), all deterministic."""
+    from bm25mi import synth
+    cfg = synth.Config("t", 60_000, 900, 300_000, 8, 6, 10)
+    a = synth.make_index(cfg)
+    u = synth.make_index(synth.Config(*list(cfg.__dict__.values())[:-1], weights="uniform"))
+    assert np.array_equal(a[0], u[0]) and np.array_equal(a[1], u[1])
+    assert u[2].min() >= 0.05 and u[2].max() <= 3.0 and not np.array_equal(a[2], u[2])
+    ip, ix, tf = synth._fill(cfg, 0, None, 0, synth.WEIGHTS["tf"])
+    assert np.array_equal(ip, a[0]) and np.all(tf >= 1) and np.all(tf == np.round(tf))
+    assert abs(float(tf.mean()) - 1.6) < 0.02
+    assert np.array_equal(tf, synth._fill(cfg, 0, None, 0, synth.WEIGHTS["tf"])[2])
