@@ -188,6 +188,27 @@ int bm25_scores_dense(bm25_index* idx, const int32_t* query, int64_t T,
                       float* out_scores);
 
 /*
+ * bm25.BM25's float64 path (the dense model's API keeps the reference's
+ * precision).  bm25_index_set_values_f64 keeps a float64 copy of the index's
+ * values beside it (the same CSC order; bm25_build_scores method 1 returns
+ * them as out_data64 — the reference's bm25_matrix entries).
+ *   bm25_scores_dense_f64: every document's float64 sum over the query's
+ *     valid ids in query order from 0 — numpy's np.sum(bm25_matrix[:, ids],
+ *     axis=1) bit for bit (column by column; a one-document corpus: numpy's
+ *     pairwise order).  Replaces BM25.get_scores (bm25.py:124-145).
+ *   bm25_topn_f64: the n best documents of those sums by (score desc, doc
+ *     asc), 0 <= n <= n_docs.  Replaces the ranking of BM25.get_top_n
+ *     (bm25.py:147-178: argsort(scores)[::-1][:n]; its order among equal
+ *     scores is numpy-implementation-defined).
+ * Errors: EINVAL when no float64 values were set, a token id >= n_terms
+ * (bm25_native's message), n out of range.
+ */
+int bm25_index_set_values_f64(bm25_index* idx, const double* data64);
+int bm25_scores_dense_f64(bm25_index* idx, const int32_t* query, int64_t T, double* out_scores);
+int bm25_topn_f64(bm25_index* idx, const int32_t* query, int64_t T, int64_t n, int32_t* out_docs,
+                  double* out_scores);
+
+/*
  * Merge W per-shard top-k lists (global doc ids) into one top-k, device
  * buffers: d_docs/d_scores are [W, Q, k], outputs [Q, k].  Used after the
  * RCCL all-gather of the doc-sharded search; the order rule

@@ -6,18 +6,16 @@ tokenisation) and builds the BM25 matrix on the MI355X with
 ``bm25_build_scores`` (bm25.py:106-121: Robertson idf + 1, ``(k1 + 1)``
 numerator, the reference's float64 arithmetic and operation order), which
 returns the CSC index data and the float64 entries of the reference's dense
-``bm25_matrix``; ``get_scores`` / ``get_top_n`` (bm25.py:124-178) then run
-through libbm25mi's kernels (dense per-document scores / batched top-k).
+``bm25_matrix``; the float64 values stay on the device beside the index.
 
-Numerics: the engine sums the query terms' scores in fp32 (the values cast
-from the float64 matrix), in query order, where the reference sums float64
-columns with numpy; scores agree to ~1e-7 relative (north_star tolerance
-1e-4) and are returned as float64 arrays like the reference's.  Documents with
-equal scores are ranked by index ascending (the reference's
-``argsort(...)[::-1]`` order among ties is implementation-defined).
-``get_top_n`` runs the engine's batched top-k for every n (above 4096 the
-exact large-k path, bm25mi_large.hip; the reference, bm25.py:172-178, ranks
-every document).
+Numerics: the reference's own precision.  ``get_scores`` is the device's
+float64 sum of the query's columns in query order (numpy's column-by-column
+reduction of ``np.sum(bm25_matrix[:, ids], axis=1)``, bm25.py:143) — the same
+bits; ``get_top_n`` ranks those float64 sums on the device (a stable radix
+sort, bm25.py:172-176's ``argsort(...)[::-1]``) — documents with equal scores
+by index ascending, where the reference's order among ties is
+numpy-implementation-defined.  (bm25_native.BM25v's fp32 CSC scorer is the
+engine's batched path; this model keeps float64 like the reference's.)
 """
 from __future__ import annotations
 
@@ -109,6 +107,7 @@ class BM25:
         self.tf = sp.csc_matrix((tfs, (docs, terms)), shape=shape).toarray()
         self.bm25_matrix = sp.csc_matrix((data64, indices, indptr), shape=shape).toarray()
         self._gpu = GpuIndex(indptr, indices, data, self.corpus_size, device=self.device)
+        self._gpu.set_values_f64(data64)  # get_scores / get_top_n rank in float64
 
     # --------------------------------------------------------------- scoring
     def _query_ids(self, query):
@@ -122,7 +121,7 @@ class BM25:
         ids = self._query_ids(query)
         if not ids:
             return np.zeros(self.corpus_size)
-        return self._gpu.scores_dense(np.asarray(ids, np.int32)).astype(np.float64)
+        return self._gpu.scores_dense_f64(np.asarray(ids, np.int32))
 
     def get_top_n(self, query, corpus, n=5):
         """bm25.py:147-178: [(score, document)] of the n best documents, best
@@ -133,7 +132,5 @@ class BM25:
             return []
         num = min(n, self.corpus_size)
         ids = self._query_ids(query)
-        q = np.full((1, max(len(ids), 1)), -1, np.int32)
-        q[0, :len(ids)] = ids
-        docs, scores = self._gpu.search(q, num)
-        return [(np.float64(s), corpus[int(d)]) for d, s in zip(docs[0], scores[0])]
+        docs, scores = self._gpu.topn_f64(np.asarray(ids, np.int32), num)
+        return [(np.float64(s), corpus[int(d)]) for d, s in zip(docs, scores)]

@@ -58,6 +58,9 @@ _SIGS = {
     "bm25_search_device": ([_P, _P, _I64, _I64, _I32, _P, _P, _P], ctypes.c_int),
     "bm25_max_token_device": ([_P, _P, _I64, _I64, _P, _P], ctypes.c_int),
     "bm25_scores_dense": ([_P, _P, _I64, _P], ctypes.c_int),
+    "bm25_index_set_values_f64": ([_P, _P], ctypes.c_int),
+    "bm25_scores_dense_f64": ([_P, _P, _I64, _P], ctypes.c_int),
+    "bm25_topn_f64": ([_P, _P, _I64, _I64, _P, _P], ctypes.c_int),
     "bm25_merge_topk_device": ([ctypes.c_int, _P, _P, _I64, _I64, _I32, _P, _P, _P],
                                ctypes.c_int),
     "bm25_merge_sorted_device": ([ctypes.c_int, _P, _P, _I64, _I64, _I32, _I64, _P, _P, _P],

@@ -18,7 +18,8 @@ REPO = os.path.dirname(os.path.dirname(PKG_DIR))
 LIB = os.path.join(PKG_DIR, "libbm25mi.so")
 SYNTH_LIB = os.path.join(PKG_DIR, "libbm25synth.so")
 
-HIP_SOURCES = ["bm25mi_kernels.hip", "bm25mi_large.hip", "bm25mi_build.hip", "bm25mi_capi.cpp"]
+HIP_SOURCES = ["bm25mi_kernels.hip", "bm25mi_large.hip", "bm25mi_build.hip", "bm25mi_sort.hip",
+               "bm25mi_dense.hip", "bm25mi_capi.cpp"]
 ARCH = os.environ.get("BM25_OFFLOAD_ARCH", "gfx950")
 
 

@@ -188,6 +188,31 @@ class GpuIndex:
         check(lib.bm25_scores_dense(self._h, _ptr(q), q.size, _ptr(out)))
         return out
 
+    # ------------------------------------------- bm25.BM25's float64 path
+    def set_values_f64(self, data64) -> None:
+        """Keep a float64 copy of the values (same CSC order) on the device
+        (bm25_index_set_values_f64)."""
+        d = np.ascontiguousarray(data64, dtype=np.float64)
+        if d.size < self.nnz:
+            raise ValueError("data64 shorter than nnz")
+        check(lib.bm25_index_set_values_f64(self._h, _ptr(d)))
+
+    def scores_dense_f64(self, query) -> np.ndarray:
+        """float64 sums of every document in query order (numpy's
+        np.sum(matrix[:, ids], axis=1), bm25.py:143)."""
+        q = np.ascontiguousarray(np.asarray(query).ravel(), dtype=np.int32)
+        out = np.zeros(self.n_docs, np.float64)
+        check(lib.bm25_scores_dense_f64(self._h, _ptr(q), q.size, _ptr(out)))
+        return out
+
+    def topn_f64(self, query, n: int) -> Tuple[np.ndarray, np.ndarray]:
+        """The n best documents of those float64 sums, (score desc, doc asc)."""
+        q = np.ascontiguousarray(np.asarray(query).ravel(), dtype=np.int32)
+        docs = np.zeros(max(int(n), 0), np.int32)
+        scores = np.zeros(max(int(n), 0), np.float64)
+        check(lib.bm25_topn_f64(self._h, _ptr(q), q.size, int(n), _ptr(docs), _ptr(scores)))
+        return docs, scores
+
     # ------------------------------------------------------------------
     def profile_enable(self, on: bool = True) -> None:
         check(lib.bm25_profile_enable(self._h, int(on)))

@@ -3,8 +3,8 @@
 // row 2: the step upstream of the path).
 //
 //   1. validate + pack keys  term << 32 | doc           (one thread per triple)
-//   2. radix sort (hipCUB) of the keys with the triple ordinal as payload:
-//      term-major, doc-ascending = canonical CSC order
+//   2. radix sort of the keys with the triple ordinal as payload
+//      (bm25mi_sort.hip): term-major, doc-ascending = canonical CSC order
 //   3. document frequencies (atomic count per term) + duplicate detection
 //   4. idf per term, unless the caller passes it
 //   5. per-posting score, written as CSC indices/data (+ optional f64 data)
@@ -25,7 +25,7 @@
 // No FMA contraction anywhere in the formulas (#pragma clang fp contract(off)).
 #include "bm25mi_internal.h"
 
-#include <hipcub/hipcub.hpp>
+#include <algorithm>
 
 namespace bm25mi {
 
@@ -172,17 +172,14 @@ hipError_t build_scores(int64_t n_docs, int64_t n_terms, int64_t n, const int32_
     BTRY(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     BTRY(hipStreamSynchronize(st));
     if (herr & 1) return done(hipSuccess);
-    hipcub::DoubleBuffer<uint64_t> kb(keys, keys2);
-    hipcub::DoubleBuffer<uint32_t> ob(ord, ord2);
-    BTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, kb, ob, (int)n, 0, end_bit, st));
-    tmp_bytes = b1;
-    BTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, df, (unsigned long long*)d_indptr,
-                                          (int)(n_terms + 1), st));
-    tmp_bytes = std::max(tmp_bytes, b2);
+    b1 = radix_sort_scratch_bytes(n);
+    b2 = exclusive_scan_scratch_bytes(n_terms + 1);
+    tmp_bytes = std::max(b1, b2);
     BTRY(hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)));
-    BTRY(hipcub::DeviceRadixSort::SortPairs(tmp, b1, kb, ob, (int)n, 0, end_bit, st));
-    const uint64_t* sk = kb.Current();
-    const uint32_t* so = ob.Current();
+    bool alt = false;
+    BTRY(radix_sort_pairs(keys, ord, keys2, ord2, n, 0, end_bit, false, 0, tmp, &alt, st));
+    const uint64_t* sk = alt ? keys2 : keys;
+    const uint32_t* so = alt ? ord2 : ord;
     hipLaunchKernelGGL(count_terms_kernel, dim3(grid_for(n)), dim3(256), 0, st, sk, n, n_terms,
                        df, d_err);
     BTRY(hipGetLastError());
@@ -203,8 +200,7 @@ hipError_t build_scores(int64_t n_docs, int64_t n_terms, int64_t n, const int32_
                          so, d_tfs, d_doc_len, w, n, n_docs, n_terms, avgdl, k1, b, d_indices, d_data,
                          d_data64);
     BTRY(hipGetLastError());
-    BTRY(hipcub::DeviceScan::ExclusiveSum(tmp, b2, df, (unsigned long long*)d_indptr,
-                                          (int)(n_terms + 1), st));
+    BTRY(exclusive_scan_u64(df, d_indptr, n_terms + 1, tmp, st));
   } else {
     BTRY(hipMemsetAsync(d_indptr, 0, sizeof(int64_t) * (n_terms + 1), st));
   }

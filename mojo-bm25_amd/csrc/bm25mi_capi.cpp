@@ -933,6 +933,101 @@ int bm25_scores_dense(bm25_index* h, const int32_t* query, int64_t T, float* out
   return BM25_OK;
 }
 
+int bm25_index_set_values_f64(bm25_index* h, const double* data64) {
+  if (!h || (h->ix.nnz > 0 && !data64)) return fail(BM25_EINVAL, "NULL argument");
+  if (!h->arrays) return fail(BM25_EINVAL, "unbuilt index");
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  if (!h->ix.val64) {
+    HIP_TRY(hipMalloc(&h->ix.val64, sizeof(double) * std::max<int64_t>(h->ix.nnz, 1)),
+            "hipMalloc(val64)");
+    h->arrays->p.push_back(h->ix.val64);  // freed with the index arrays
+  }
+  if (h->ix.nnz > 0)
+    HIP_TRY(hipMemcpyAsync(h->ix.val64, data64, sizeof(double) * h->ix.nnz, hipMemcpyHostToDevice,
+                           h->stream), "H2D val64");
+  HIP_TRY(hipStreamSynchronize(h->stream), "val64 sync");
+  return BM25_OK;
+}
+
+// Device query + f64 dense sums of one query on h's stream (caller holds
+// h->mu and has set the device); *d_q / *d_out are freed by the caller.
+static int dense_f64_query(bm25_index* h, const int32_t* query, int64_t T, int32_t** d_q,
+                           double** d_out) {
+  if (T < 0) return fail(BM25_EINVAL, "negative query length");
+  if (T > 0 && !query) return fail(BM25_EINVAL, "NULL query");
+  if (!h->ix.val64) return fail(BM25_EINVAL, "no float64 values: bm25_index_set_values_f64 first");
+  int64_t mx = 0;
+  for (int64_t i = 0; i < T; ++i) mx = std::max<int64_t>(mx, query[i]);
+  if (mx >= h->ix.n_terms)
+    return fail(BM25_EINVAL,
+                "The maximum token ID in the query (%lld) is higher than the number of tokens in "
+                "the index.",
+                (long long)mx);
+  HIP_TRY(hipMalloc(d_q, sizeof(int32_t) * std::max<int64_t>(T, 1)), "hipMalloc(query)");
+  HIP_TRY(hipMalloc(d_out, sizeof(double) * std::max<int64_t>(h->ix.n_docs, 1)), "hipMalloc(dense)");
+  if (T > 0)
+    HIP_TRY(hipMemcpyAsync(*d_q, query, sizeof(int32_t) * T, hipMemcpyHostToDevice, h->stream),
+            "H2D query");
+  HIP_TRY(launch_dense_f64(h->ix, h->ix.val64, *d_q, T, *d_out, h->stream), "dense f64 launch");
+  return BM25_OK;
+}
+
+int bm25_scores_dense_f64(bm25_index* h, const int32_t* query, int64_t T, double* out_scores) {
+  if (!h || !out_scores) return fail(BM25_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  int32_t* d_q = nullptr;
+  double* d_out = nullptr;
+  int rc = dense_f64_query(h, query, T, &d_q, &d_out);
+  hipError_t e = hipSuccess;
+  if (rc == BM25_OK && h->ix.n_docs > 0)
+    e = hipMemcpyAsync(out_scores, d_out, sizeof(double) * h->ix.n_docs, hipMemcpyDeviceToHost,
+                       h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  hipFree(d_q);
+  hipFree(d_out);
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(e, "scores_dense_f64");
+  return BM25_OK;
+}
+
+int bm25_topn_f64(bm25_index* h, const int32_t* query, int64_t T, int64_t n, int32_t* out_docs,
+                  double* out_scores) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (n < 0 || n > h->ix.n_docs)
+    return fail(BM25_EINVAL, "n=%lld must be in 0..n_docs (%lld)", (long long)n,
+                (long long)h->ix.n_docs);
+  if (n > 0 && (!out_docs || !out_scores)) return fail(BM25_EINVAL, "NULL output");
+  if (n == 0) return BM25_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  int32_t* d_q = nullptr;
+  double* d_out = nullptr;
+  void* scratch = nullptr;
+  int32_t* d_docs = nullptr;
+  double* d_sc = nullptr;
+  int rc = dense_f64_query(h, query, T, &d_q, &d_out);
+  hipError_t e = hipSuccess;
+  if (rc == BM25_OK) {
+    e = hipMalloc(&scratch, topn_f64_scratch_bytes(h->ix.n_docs));
+    if (e == hipSuccess) e = hipMalloc(&d_docs, sizeof(int32_t) * n);
+    if (e == hipSuccess) e = hipMalloc(&d_sc, sizeof(double) * n);
+    if (e == hipSuccess)
+      e = launch_topn_f64(d_out, h->ix.n_docs, n, scratch, d_docs, d_sc, h->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(out_docs, d_docs, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(out_scores, d_sc, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  else hipStreamSynchronize(h->stream);
+  for (void* p : {(void*)d_q, (void*)d_out, scratch, (void*)d_docs, (void*)d_sc}) hipFree(p);
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(e, "topn_f64");
+  return BM25_OK;
+}
+
 int bm25_merge_topk_device(int device, const int32_t* d_docs, const float* d_scores, int64_t W,
                            int64_t Q, int32_t k, int32_t* d_out_docs, float* d_out_scores,
                            void* stream) {

@@ -118,6 +118,7 @@ struct DevIndex {
   int64_t n_pairs = 0;
   uint16_t* ldoc = nullptr;
   float* val = nullptr;
+  double* val64 = nullptr;  // float64 values of the same postings (bm25.BM25's path; optional)
   // Tile bounds (dense segment table, non-negative index): each (term,
   // tile)'s largest score as f16 bits rounded DOWN, [V][bmax_stride] — a lower
   // bound of that score (threshold keys) and, one f16 step up, an upper bound
@@ -267,6 +268,35 @@ hipError_t launch_max_token(const int32_t* d_queries, int64_t n, int32_t* d_out,
 // Tile shifts with compiled kernels, and the one a new index takes.
 bool tile_shift_supported(int s);
 int build_tile_shift();
+
+// Device sort and scan (bm25mi_sort.hip; hand-written, no hipCUB).
+// Stable LSD radix sort of n (u64 key, u32 value) pairs: by the key bits
+// [key_bits_lo, key_bits_hi) (descending: of ~key), then by the value bits
+// [0, val_bits_hi) (vals may be null when val_bits_hi == 0).  keys_alt /
+// vals_alt are same-sized buffers; *result_in_alt tells which pair of buffers
+// holds the result.  scratch: radix_sort_scratch_bytes(n) bytes.
+size_t radix_sort_scratch_bytes(int64_t n);
+hipError_t radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, uint32_t* vals_alt,
+                            int64_t n, int key_bits_lo, int key_bits_hi, bool descending,
+                            int val_bits_hi, void* scratch, bool* result_in_alt, hipStream_t st);
+// G rows of n keys each ([G][n]), every row sorted descending in place of
+// the segmented sort (rows / rows_alt: G * n u32 of scratch values).
+hipError_t radix_sort_rows_desc(uint64_t* keys, uint64_t* keys_alt, uint32_t* rows,
+                                uint32_t* rows_alt, int64_t G, int64_t n, void* scratch,
+                                bool* result_in_alt, hipStream_t st);
+// out[i] = in[0] + ... + in[i - 1] (out[0] = 0) for n u64 counts.
+size_t exclusive_scan_scratch_bytes(int64_t n);
+hipError_t exclusive_scan_u64(const unsigned long long* in, int64_t* out, int64_t n, void* scratch,
+                              hipStream_t st);
+
+// bm25.BM25's float64 path (bm25mi_dense.hip): dense sums of one query from
+// the index's float64 values (numpy's order), and the n best of a dense
+// float64 vector by (score desc, doc asc).
+hipError_t launch_dense_f64(const DevIndex& ix, const double* val64, const int32_t* d_query,
+                            int64_t T, double* d_out, hipStream_t st);
+size_t topn_f64_scratch_bytes(int64_t n_docs);
+hipError_t launch_topn_f64(const double* d_scores, int64_t n_docs, int64_t n, void* scratch,
+                           int32_t* d_docs, double* d_out_scores, hipStream_t st);
 
 // GPU index build (bm25mi_build.hip): scoring rules of bm25_build_scores.
 enum { kLucene = 0, kBm25Py = 1 };

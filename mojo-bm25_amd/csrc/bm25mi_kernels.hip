@@ -788,6 +788,10 @@ constexpr int kQW = 4;
 #define BM25_FLAT_WPE 5
 #endif
 
+#ifndef BM25_CLAMP  // row loads of idle lanes kept inside the row's valid lanes
+#define BM25_CLAMP 0
+#endif
+
 // Inclusive prefix sum over the wave (DPP: rows of 16, then the row carries).
 __device__ __forceinline__ uint32_t scan64(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
@@ -1154,7 +1158,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     if (il == nI) next_chunk();
     const uint32_t base = lane_u32(tI.base, (int)il);
     wR[s] = lane_u32(tI.w, (int)il);
+#if BM25_CLAMP
+    // lanes past the row's last valid one load that lane's pair again: the
+    // row touches no cache line beyond its segment's (a short segment's row
+    // would otherwise pull in 768 B of other segments' postings)
+    const uint32_t wv = wR[s];
+    const uint32_t top = max(row_lo(wv) + row_n0(wv), row_n1(wv));
+    const uint32_t t4 = (top > 0u ? top - 1u : 0u) * 4u;
+    const uint32_t lo4 = min(lane * 4u, t4), lo8 = min(lane * 8u, 2u * t4);
+#else
     const uint32_t lo4 = lane * 4u, lo8 = lane * 8u;
+#endif
     ldR[s] = __builtin_amdgcn_raw_buffer_load_b32(pr.ldoc, (int)lo4, (int)base, 0);
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)lo8, (int)(base * 2u), 0);
     v0R[s] = __uint_as_float((uint32_t)v[0]);

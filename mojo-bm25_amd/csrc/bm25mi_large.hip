@@ -17,8 +17,8 @@
 //                               a query is decided as soon as every key with
 //                               its prefix is needed (usually 4-5 passes)
 //   3. lk_compact_kernel        the k keys >= the k-th key (unordered)
-//   4. segmented radix sort     hipCUB, descending (per-query device sort for
-//                               very long rows)
+//   4. row sort                 descending, every row of the chunk in one
+//                               sequence of radix passes (bm25mi_sort.hip)
 //   5. lk_write_kernel          keys -> doc ids (+ doc_offset) and scores;
 //                               rows of a shard with fewer than k docs are
 //                               padded with doc -1 / score bits ~0
@@ -27,8 +27,6 @@
 // the engine (bm25mi_internal.h), so equal scores order by doc ascending and
 // zero-score (untouched) documents fill a row the same way.
 #include "bm25mi_internal.h"
-
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <vector>
@@ -261,11 +259,6 @@ __global__ __launch_bounds__(256) void lk_list_keys_kernel(const int32_t* __rest
   }
 }
 
-__global__ __launch_bounds__(64) void lk_offsets_kernel(int* __restrict__ off, int64_t G,
-                                                        int64_t n) {
-  for (int64_t g = threadIdx.x; g <= G; g += 64) off[g] = (int)(g * n);
-}
-
 // Sorted rows [G][n] -> the first k of each: docs (+ doc_offset) and scores
 // of rows q0 .. q0 + G; positions >= k_valid, and key 0, are padding.
 __global__ __launch_bounds__(256) void lk_write_kernel(const uint64_t* __restrict__ keys,
@@ -287,33 +280,23 @@ __global__ __launch_bounds__(256) void lk_write_kernel(const uint64_t* __restric
   }
 }
 
-// Rows longer than this are sorted one by one with the device-wide radix
-// sort (the segmented sort gives a row one workgroup).
-constexpr int64_t kSegSortMax = 1 << 20;
-
-// Temporary bytes of sorting G rows of n keys (descending).
-hipError_t sort_bytes(int64_t G, int64_t n, size_t* bytes) {
-  *bytes = 0;
-  if (n > kSegSortMax)
-    return hipcub::DeviceRadixSort::SortKeysDescending(nullptr, *bytes, (const uint64_t*)nullptr,
-                                                       (uint64_t*)nullptr, (int)n, 0, 64, 0);
-  return hipcub::DeviceSegmentedRadixSort::SortKeysDescending(
-      nullptr, *bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(G * n), (int)G,
-      (const int*)nullptr, (const int*)nullptr, 0, 64, 0);
+// Scratch bytes of sorting G rows of n keys (descending): the radix passes'
+// histograms + the row numbers (two buffers).
+int64_t sort_bytes(int64_t G, int64_t n) {
+  return (int64_t)radix_sort_scratch_bytes(G * n) + 8 * G * n;
 }
 
-hipError_t sort_rows(const uint64_t* in, uint64_t* out, int64_t G, int64_t n, const int* off,
-                     void* tmp, size_t bytes, hipStream_t st) {
-  if (n > kSegSortMax) {
-    for (int64_t g = 0; g < G; ++g) {
-      const hipError_t e = hipcub::DeviceRadixSort::SortKeysDescending(
-          tmp, bytes, in + g * n, out + g * n, (int)n, 0, 64, st);
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-  }
-  return hipcub::DeviceSegmentedRadixSort::SortKeysDescending(tmp, bytes, in, out, (int)(G * n),
-                                                              (int)G, off, off + 1, 0, 64, st);
+// Sorts rows [G][n] of `in` descending; *out = the buffer that holds them
+// (in or alt).
+hipError_t sort_rows(uint64_t* in, uint64_t* alt, int64_t G, int64_t n, char* tmp,
+                     const uint64_t** out, hipStream_t st) {
+  uint32_t* rows = (uint32_t*)tmp;
+  uint32_t* rows_alt = rows + G * n;
+  bool in_alt = false;
+  const hipError_t e =
+      radix_sort_rows_desc(in, alt, rows, rows_alt, G, n, rows_alt + G * n, &in_alt, st);
+  *out = in_alt ? alt : in;
+  return e;
 }
 
 // Device memory this path may take per launch sequence.
@@ -362,30 +345,25 @@ hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int
     return hipMemsetAsync(d_scores, 0xFF, sizeof(float) * Q * k, st);
   }
   const int64_t Np = ix.ntiles << ix.tile_shift;  // row stride: whole tiles
-  size_t sb1 = 0;
-  LK_TRY(sort_bytes(1, kv, &sb1));
-  const int64_t per_q = Np * 4 + (int64_t)kv * 16 + 256 * 4 + 64 + (int64_t)sb1 / 4;
+  const int64_t per_q = Np * 4 + (int64_t)kv * 16 + 256 * 4 + 64 + sort_bytes(1, kv);
   int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));
   G = std::min<int64_t>(G, 65535);
   G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / kv - 1));
-  size_t sb = 0;
-  LK_TRY(sort_bytes(G, kv, &sb));
+  const int64_t sb = sort_bytes(G, kv);
   Scratch sc(st);
   float* scores = nullptr;
   uint32_t* hist = nullptr;
   SelState* state = nullptr;
   int32_t* cnt = nullptr;
-  uint64_t *keys = nullptr, *sorted = nullptr;
-  int* off = nullptr;
-  void* tmp = nullptr;
+  uint64_t *keys = nullptr, *alt = nullptr;
+  char* tmp = nullptr;
   LK_TRY(sc.get(&scores, G * Np));
   LK_TRY(sc.get(&hist, G * 256));
   LK_TRY(sc.get(&state, G));
   LK_TRY(sc.get(&cnt, G));
   LK_TRY(sc.get(&keys, G * kv));
-  LK_TRY(sc.get(&sorted, G * kv));
-  LK_TRY(sc.get(&off, G + 1));
-  LK_TRY(sc.get((char**)&tmp, (int64_t)sb));
+  LK_TRY(sc.get(&alt, G * kv));
+  LK_TRY(sc.get(&tmp, sb));
   LK_TRY(hipMemsetAsync(hist, 0, sizeof(uint32_t) * G * 256, st));
   const int64_t n4 = (ix.n_docs + 3) >> 2;
   for (int64_t q0 = 0; q0 < Q; q0 += G) {
@@ -400,8 +378,8 @@ hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int
     }
     hipLaunchKernelGGL(lk_compact_kernel, grid, dim3(256), 0, st, scores, Np, ix.n_docs, state, cnt,
                        keys, (int64_t)kv);
-    hipLaunchKernelGGL(lk_offsets_kernel, dim3(1), dim3(64), 0, st, off, g, (int64_t)kv);
-    LK_TRY(sort_rows(keys, sorted, g, kv, off, tmp, sb, st));
+    const uint64_t* sorted = nullptr;
+    LK_TRY(sort_rows(keys, alt, g, kv, tmp, &sorted, st));
     hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(g * k, 256, 4096)), dim3(256), 0, st, sorted,
                        (int64_t)kv, g, k, kv, ix.doc_offset, d_docs + q0 * k, d_scores + q0 * k);
     LK_TRY(hipGetLastError());
@@ -415,27 +393,22 @@ hipError_t launch_merge_large(const int32_t* d_docs, const float* d_scores, int6
   if (Q == 0 || k == 0) return hipSuccess;
   const int64_t n = W * (int64_t)k;
   if (n > INT32_MAX / 2) return hipErrorInvalidValue;
-  size_t sb1 = 0;
-  LK_TRY(sort_bytes(1, n, &sb1));
-  const int64_t per_q = n * 16 + 64 + (int64_t)sb1 / 4;
+  const int64_t per_q = n * 16 + 64 + sort_bytes(1, n);
   int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));
   G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / n - 1));
-  size_t sb = 0;
-  LK_TRY(sort_bytes(G, n, &sb));
+  const int64_t sb = sort_bytes(G, n);
   Scratch sc(st);
-  uint64_t *keys = nullptr, *sorted = nullptr;
-  int* off = nullptr;
-  void* tmp = nullptr;
+  uint64_t *keys = nullptr, *alt = nullptr;
+  char* tmp = nullptr;
   LK_TRY(sc.get(&keys, G * n));
-  LK_TRY(sc.get(&sorted, G * n));
-  LK_TRY(sc.get(&off, G + 1));
-  LK_TRY(sc.get((char**)&tmp, (int64_t)sb));
+  LK_TRY(sc.get(&alt, G * n));
+  LK_TRY(sc.get(&tmp, sb));
   for (int64_t q0 = 0; q0 < Q; q0 += G) {
     const int64_t g = std::min<int64_t>(G, Q - q0);
     hipLaunchKernelGGL(lk_list_keys_kernel, dim3(grid_for(g * n, 256, 8192)), dim3(256), 0, st,
                        d_docs, d_scores, W, q0, g, k, rank_stride, keys);
-    hipLaunchKernelGGL(lk_offsets_kernel, dim3(1), dim3(64), 0, st, off, g, n);
-    LK_TRY(sort_rows(keys, sorted, g, n, off, tmp, sb, st));
+    const uint64_t* sorted = nullptr;
+    LK_TRY(sort_rows(keys, alt, g, n, tmp, &sorted, st));
     hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(g * k, 256, 4096)), dim3(256), 0, st, sorted,
                        n, g, k, k, 0ll, d_out_docs + q0 * k, d_out_scores + q0 * k);
     LK_TRY(hipGetLastError());

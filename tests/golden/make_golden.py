@@ -13,6 +13,8 @@ Fixtures
                  bm25_test.py:23 through vocab.index.json, outputs of
                  BM25v.search, plus the two error messages
   main_demo.npz  bm25_native.py:219-248 (2x3 dense -> CSC, query [[0,1]], k=1)
+  bm25_near_ties.npz  a seeded corpus + queries where the reference's float64
+                 ranking differs from fp32 sums' (bm25.BM25 must rank in f64)
   bm25_dense.npz the reference's dense BM25 model (bm25.py:6-178) fitted on
                  its own __main__ corpus (bm25.py:182-196): bm25_matrix, and
                  get_scores / get_top_n(n=5) of a few queries (OOV, duplicate
@@ -193,7 +195,49 @@ def bm25_dense():
     np.savez(os.path.join(OUT, "bm25_dense.npz"), **out)
 
 
+def bm25_near_ties():
+    """bm25_near_ties.npz: a seeded random corpus (2000 docs over 30 words) and
+    queries whose float64 ranking (the reference's get_top_n) differs from the
+    ranking of the same sums in fp32: two documents whose float64 scores are
+    distinct but round to one fp32 value (found by search, seed 2024)."""
+    import bm25 as ref_bm25
+    rng = np.random.default_rng(2024)
+    words = [f"w{i}" for i in range(30)]
+    for attempt in range(200):
+        corpus = [list(rng.choice(words, size=int(rng.integers(3, 12)))) for _ in range(2000)]
+        model = ref_bm25.BM25()
+        model.fit(corpus)
+        m32 = model.bm25_matrix.astype(np.float32)
+        ar = np.arange(len(corpus))
+        hits, queries = [], []
+        for _ in range(40):
+            q = [str(w) for w in rng.choice(words, size=int(rng.integers(2, 6)))]
+            s64 = model.get_scores(q)
+            s32 = np.zeros(len(corpus), np.float32)
+            for t in q:
+                s32 = s32 + m32[:, model.term_to_id[t]]
+            o64 = np.lexsort((ar, -s64))[:20]
+            o32 = np.lexsort((ar, -s32.astype(np.float64)))[:20]
+            vals, c = np.unique(s64, return_counts=True)
+            rep = dict(zip(vals.tolist(), c.tolist()))
+            if any(o64[j] != o32[j] and rep[s64[o64[j]]] == 1 for j in range(20)):
+                hits.append(len(queries))
+            queries.append(" ".join(q))
+        if hits:
+            break
+    out = {"docs": np.array([" ".join(d) for d in corpus]), "queries": np.array(queries),
+           "fp32_differs": np.array(hits, np.int64)}
+    for i, q in enumerate(queries):
+        toks = q.split()
+        out[f"scores_{i}"] = np.asarray(model.get_scores(toks))
+        top = model.get_top_n(toks, corpus, n=20)
+        out[f"top_scores_{i}"] = np.array([t[0] for t in top], np.float64)
+        out[f"top_docs_{i}"] = np.array([corpus.index(t[1]) for t in top], np.int64)
+    np.savez_compressed(os.path.join(OUT, "bm25_near_ties.npz"), **out)
+
+
 if __name__ == "__main__":
+    bm25_near_ties()
     bm25_dense()
     animal()
     main_demo()

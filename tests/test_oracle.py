@@ -186,3 +186,53 @@ def test_build_scores_bm25py_restatement_matches_reference_matrix():
                                                "bm25py", np.mean(dl))
     m = sp.csc_matrix((d64, ix, ip), shape=(len(corpus), len(tid))).toarray()
     assert np.array_equal(m, g["bm25_matrix"])
+
+
+def _bm25_corpus_csc(docs_text, vocab=None):
+    """The bm25.py matrix (build_scores_numpy "bm25py") of a text corpus as
+    CSC with its float64 values; vocab = sorted words (bm25.py:73)."""
+    from collections import Counter
+    corpus = [d.lower().split() for d in docs_text]
+    vocab = sorted({t for d in corpus for t in d}) if vocab is None else vocab
+    tid = {t: i for i, t in enumerate(vocab)}
+    docs, terms, tfs = [], [], []
+    for i, d in enumerate(corpus):
+        for t, c in Counter(d).items():
+            docs.append(i), terms.append(tid[t]), tfs.append(c)
+    dl = [len(d) for d in corpus]
+    ip, ix, _, d64 = oracle.build_scores_numpy(docs, terms, tfs, dl, len(vocab), 1.5, 0.75,
+                                               "bm25py", float(np.mean(dl)))
+    return corpus, tid, ip, ix, d64
+
+
+@pytest.mark.parametrize("name", ["bm25_dense.npz", "bm25_near_ties.npz"])
+def test_bm25_f64_scores_restatement_matches_reference(name):
+    """oracle.scores_f64 (bm25.py:143's column-by-column float64 sum, restated
+    on the CSC) reproduces the reference's get_scores bit for bit, and
+    oracle.topn_f64 its get_top_n scores — on the reference's own corpus and on
+    the near-tie corpus whose fp32 ranking differs from float64's."""
+    g = np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+    corpus, tid, ip, ix, d64 = _bm25_corpus_csc(g["docs"].tolist())
+    for i, q in enumerate(g["queries"].tolist()):
+        ids = [tid[t] for t in q.lower().split() if t in tid]
+        s = oracle.scores_f64(len(corpus), ip, ix, d64, ids)
+        assert np.array_equal(s.view(np.uint64), g[f"scores_{i}"].view(np.uint64)), (name, q)
+        n = len(g[f"top_scores_{i}"])
+        d, sc = oracle.topn_f64(s, n)
+        assert np.array_equal(sc, g[f"top_scores_{i}"])
+    if name == "bm25_near_ties.npz":
+        assert len(g["fp32_differs"]) > 0
+
+
+def test_bm25_f64_one_document_corpus_is_pairwise():
+    """A one-document corpus: numpy sums the one gathered row pairwise (T >=
+    8 differs from the in-order sum), and the restatement follows it."""
+    rng = np.random.default_rng(3)
+    v = rng.random(40) * 7
+    ip = np.arange(41, dtype=np.int64)
+    ix = np.zeros(40, np.int32)
+    for T in (3, 8, 9, 17, 40):
+        ids = list(rng.integers(0, 40, T))
+        want = np.sum(v[None, :][:, ids], axis=1)
+        got = oracle.scores_f64(1, ip, ix, v, ids)
+        assert np.array_equal(got, want), T
