@@ -72,5 +72,35 @@ def build(force: bool = False, verbose: bool = False) -> None:
         os.replace(tmp, SYNTH_LIB)
 
 
+def build_asan_check(verbose: bool = False) -> str:
+    """tests/asan/host_check built against every source with AddressSanitizer
+    on the host side (-Xarch_host -fsanitize=address; device code as usual),
+    into mojo-bm25_amd/bm25mi/_asan/ (rebuilt when a source is newer).  Test
+    infrastructure for tests/test_host.py (SURVEY.md:235), not the product."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    out = os.path.join(PKG_DIR, "_asan")
+    os.makedirs(out, exist_ok=True)
+    exe = os.path.join(out, "host_check")
+    main = os.path.join(REPO, "tests", "asan", "host_check.cpp")
+    srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES] + [main]
+    hdrs = [os.path.join(CSRC, "bm25mi_internal.h"), os.path.join(REPO, "include", "bm25mi.h")]
+    if not _stale(exe, srcs + hdrs):
+        return exe
+    flags = [f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", "-fPIC", "-w",
+             "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+    jobs, objs = [], []
+    for src in srcs:
+        o = os.path.join(out, os.path.splitext(os.path.basename(src))[0] + ".o")
+        objs.append(o)
+        jobs.append([hipcc] + flags + ["-c", "-o", o, src])
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(len(jobs)) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+    _run([hipcc, f"--offload-arch={ARCH}", "-fsanitize=address", "-fno-gpu-sanitize", "-o",
+          exe + ".tmp"] + objs, verbose)
+    os.replace(exe + ".tmp", exe)
+    return exe
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)

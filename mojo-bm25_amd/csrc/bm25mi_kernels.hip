@@ -1052,9 +1052,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
 #pragma unroll
         for (int o = 1; o < (int)TT; o <<= 1) ub += __shfl_xor(ub, o, 64);
         const bool cut = ub * 1.0001f < key_score((uint32_t)(thN >> 32));
-        if (cut && !skip && lt == 0u && (int)li < nx.bw) ++nbound;
-        // ... and their postings (lanes outside the item hold r1 == r0)
-        if (cut && !skip) npost += dN.r1 - dN.r0;
+        // ... the tile's postings (lanes outside the item hold r1 == r0), counted
+        // with the pair by the tile's first term lane
+        uint32_t tp = dN.r1 - dN.r0;
+#pragma unroll
+        for (int o = 1; o < (int)TT; o <<= 1) tp += (uint32_t)__shfl_xor((int)tp, o, 64);
+        if (cut && !skip && lt == 0u && (int)li < nx.bw) {
+          ++nbound;
+          npost += tp;
+        }
         skip = skip || cut;
       }
     }

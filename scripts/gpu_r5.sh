@@ -15,7 +15,7 @@ cd $R
 for step in ${STEPS:-tests lines}; do
   case $step in
   tests)
-    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+    timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_X--x} -v -s -p no:cacheprovider --timeout 600 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|passed|failed" $OUT/pytest_gpu.log | tail -30; [ -n "$PYTEST_CONTINUE" ] || exit 1; }
     tail -1 $OUT/pytest_gpu.log
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; tail -20 $OUT/smoke.log; exit 1; }
     ;;
