@@ -122,8 +122,9 @@ int bm25_index_bounds(const bm25_index* idx, int32_t* has_bounds, int64_t* bytes
  *   queries    [Q, T] int32, negative = padding, every id < n_terms
  *   out_docs   [Q, k] int32
  *   out_scores [Q, k] f32
- * Every 0 <= k <= n_docs is served (k > 4096 by the exact large-k path:
- * dense scores, radix selection of the k-th key, sort of the k survivors).
+ * Every 0 <= k <= n_docs is served (k > 4096 by the exact large-k path: a
+ * sampled threshold, the keys above it listed, selected and sorted — or
+ * dense score rows with a radix selection where lists cannot serve).
  * Errors: EINVAL when a token id >= n_terms (message matches
  * bm25_native.py:118-121), when k < 0 or k > n_docs.
  */
@@ -327,15 +328,17 @@ int bm25_search_stats_ex(bm25_index* idx, int64_t* rescored_tiles,
  *   stage, [2] (query, tile) pairs the REST pass skipped by their tile
  *   bound, [3] the postings of those skipped (query, tile) segments (what
  *   the skip saved of the algorithmic bytes, 8 B each), [4] queries left to
- *   the block merge (lists longer than one wavefront's registers).
- * n must be in 1..5. */
+ *   the block merge (lists longer than one wavefront's registers), [5] k >
+ *   4096: queries the list path handed to dense score rows (-1: the dense
+ *   path served the whole search).
+ * n must be in 1..6. */
 int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
 
 /*
  * Search options of one handle.  A new handle takes them from the
  * environment (BM25_FLAT, BM25_FLAT_BW, BM25_ITEMS_PER_WAVE, BM25_SAMPLE_P,
  * BM25_LIST_CAP, BM25_CLAIM_CH, BM25_CLAIM_M, BM25_TILE_BOUND, BM25_THETA_BOUND,
- * BM25_GRID_PCT) at
+ * BM25_GRID_PCT, BM25_LARGE_LISTS) at
  * bm25_index_create; these
  * calls change or read them afterwards, effective from the next search.
  * Results never depend on them (every setting is bit-exact); they choose
@@ -360,6 +363,10 @@ int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
  *                    document's score lower bound) with no SAMPLE pass;
  *                    0: the sampled threshold.  Every shard of a multi-rank
  *                    search needs the same setting (bm25_sample_width)
+ *   "large_lists"    1 (default): k > 4096 takes the list path where it
+ *                    applies (a sampled threshold, keys above it listed by the
+ *                    REST pass, selected and sorted — no dense score rows);
+ *                    0: dense score rows for every query
  *   "grid_pct"       percent of the device's resident workgroup slots the
  *                    persistent score kernels launch (1..100, default 100):
  *                    below 100 leaves slots for kernels of another stream

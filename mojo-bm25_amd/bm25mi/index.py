@@ -269,11 +269,11 @@ class GpuIndex:
         tiles re-scored exactly, queries sent to the exact fallback stage,
         (query, tile) pairs the REST pass skipped by their tile bound and the
         postings of those pairs, queries left to the block merge."""
-        v = (ctypes.c_int64 * 5)()
-        check(lib.bm25_search_counters(self._h, v, 5))
+        v = (ctypes.c_int64 * 6)()
+        check(lib.bm25_search_counters(self._h, v, 6))
         return {"rescored_tiles": v[0], "fallback_queries": v[1],
                 "bound_skipped_tiles": v[2], "bound_skipped_postings": v[3],
-                "block_merge_queries": v[4]}
+                "block_merge_queries": v[4], "large_dense_queries": v[5]}
 
 
 def merge_topk_device(device: int, d_docs, d_scores, W: int, Q: int, k: int, d_out_docs,

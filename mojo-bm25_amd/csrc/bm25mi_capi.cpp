@@ -97,6 +97,8 @@ struct bm25_index {
   int32_t* report_dev = nullptr;
   int32_t seq = 0, last_bound_seq = -1, seen_seq = -1, weak_until = 0, backoff = 64;
   int64_t last_bound_q = 0;
+  int64_t large_fallback = 0;  // queries of the last large-k list search taken by dense rows
+                               // (-1: the dense path served the whole search)
 };
 
 namespace {
@@ -139,6 +141,7 @@ SearchOpts env_opts() {
   o.tile_bound = env_int("BM25_TILE_BOUND", o.tile_bound) != 0;
   o.theta_bound = env_int("BM25_THETA_BOUND", o.theta_bound) != 0;
   o.grid_pct = std::min(100, std::max(1, env_int("BM25_GRID_PCT", o.grid_pct)));
+  o.large_lists = env_int("BM25_LARGE_LISTS", o.large_lists) != 0;
   return o;
 }
 
@@ -174,6 +177,9 @@ int set_opt(SearchOpts& o, const char* name, int64_t v) {
   } else if (n == "theta_bound") {
     if (v != 0 && v != 1) return fail(BM25_EINVAL, "theta_bound must be 0 or 1");
     o.theta_bound = (int)v;
+  } else if (n == "large_lists") {
+    if (v != 0 && v != 1) return fail(BM25_EINVAL, "large_lists must be 0 or 1");
+    o.large_lists = (int)v;
   } else if (n == "grid_pct") {
     if (v < 1 || v > 100) return fail(BM25_EINVAL, "grid_pct must be in 1..100");
     o.grid_pct = (int)v;
@@ -196,6 +202,7 @@ int get_opt(const SearchOpts& o, const char* name, int64_t* v) {
   else if (n == "tile_bound") *v = o.tile_bound;
   else if (n == "theta_bound") *v = o.theta_bound;
   else if (n == "grid_pct") *v = o.grid_pct;
+  else if (n == "large_lists") *v = o.large_lists;
   else return fail(BM25_EINVAL, "unknown option '%s'", name);
   return BM25_OK;
 }
@@ -366,6 +373,13 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
                int32_t* d_docs, float* d_scores, hipStream_t st) {
   if (Q == 0 || k == 0) return BM25_OK;
   if (k > kMaxK) {  // any k up to n_docs: the large-k path (bm25mi_large.hip)
+    // the list path when it applies (no dense score rows), else dense rows
+    const bool lists = h->ix.opt.large_lists && k <= kLargeListMaxK && k <= h->ix.n_docs &&
+                       large_list_supported(h->ix, T, Q) && large_geom(h->ix, k).P > 0;
+    if (lists) {
+      const int rc = ensure_ws(h, Q, T, 1);  // claim counters, counters, segment table
+      if (rc) return rc;
+    }
     HIP_TRY(order_ws(h, st), "workspace order");
     // this search selects without the counters: the stats read as zero, not
     // as the previous search's
@@ -375,8 +389,16 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
     h->ix.disp.sample_p = 1;
     EventPair* ev = next_events(h);
     if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
-    HIP_TRY(launch_search_large(h->ix, d_queries, Q, T, k, d_docs, d_scores, st),
-            "large-k search launch");
+    if (lists) {
+      int64_t nfb = 0;
+      HIP_TRY(launch_search_large_lists(h->ix, d_queries, Q, T, k, h->ws, d_docs, d_scores, &nfb, st),
+              "large-k list search");
+      h->large_fallback = nfb;
+    } else {
+      h->large_fallback = -1;
+      HIP_TRY(launch_search_large(h->ix, d_queries, Q, T, k, d_docs, d_scores, st),
+              "large-k search launch");
+    }
     if (ev) {
       HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
       HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
@@ -1096,14 +1118,14 @@ int bm25_search_stats_ex(bm25_index* h, int64_t* rescored_tiles, int64_t* fallba
 
 int bm25_search_counters(bm25_index* h, int64_t* out, int32_t n) {
   if (!h || !out) return fail(BM25_EINVAL, "NULL argument");
-  if (n < 1 || n > 5) return fail(BM25_EINVAL, "n=%d must be in 1..5", n);
+  if (n < 1 || n > 6) return fail(BM25_EINVAL, "n=%d must be in 1..6", n);
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
   int32_t cnt[kCounters] = {};
   read_counters(h, cnt);
   uint64_t post = 0;
   std::memcpy(&post, cnt + 6, sizeof post);  // counters[6..7]: a u64 (score_flat_kernel)
-  const int64_t v[5] = {cnt[3], cnt[2], cnt[5], (int64_t)post, cnt[4]};
+  const int64_t v[6] = {cnt[3], cnt[2], cnt[5], (int64_t)post, cnt[4], h->large_fallback};
   for (int i = 0; i < n; ++i) out[i] = v[i];
   return BM25_OK;
 }

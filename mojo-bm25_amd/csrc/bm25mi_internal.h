@@ -38,6 +38,8 @@ __host__ __device__ inline uint64_t make_key(float s, uint32_t doc) {
 
 // Exact candidates kept per sample tile.
 constexpr int kTileM = 4;
+// Keys per sample tile of the large-k list path (the best of each 256-doc slice).
+constexpr int kLargeM = 8;
 // Largest k of the sampled-threshold pipeline; larger k (up to n_docs) take
 // the large-k path (bm25mi_large.hip).
 constexpr int kMaxK = 4096;
@@ -76,6 +78,7 @@ struct SearchOpts {
   int theta_bound = 1;     // threshold keys from the tile bounds instead of a SAMPLE pass
                            // (needs bmax; search_geom)
   int grid_pct = 100;      // percent of the resident slots the persistent score kernels take
+  int large_lists = 1;     // k > kMaxK: the list path (0: dense score rows for every query)
 };
 
 // What the last search launched (bm25_search_dispatch).
@@ -254,6 +257,30 @@ hipError_t launch_scores_batch(const DevIndex& ix, const int32_t* d_queries, int
 // sequence.
 hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                                int k, int32_t* d_docs, float* d_scores, hipStream_t stream);
+// The large-k list path's passes (bm25mi_kernels.hip; used by
+// bm25mi_large.hip): SAMPLE with kLargeM keys per sample tile into keys[Q][g.S]
+// (g.m == kLargeM), and REST into the workspace's theta / list / list_cnt /
+// list_cap (the caller's buffers).  large_list_supported: the flat kernel
+// serves the batch and the index is non-negative.
+hipError_t launch_sample_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                               const SampleGeom& g, uint64_t* keys, const Workspace& ws,
+                               hipStream_t stream);
+hipError_t launch_rest_lists(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                             const SampleGeom& g, const Workspace& ws, hipStream_t stream);
+bool large_list_supported(const DevIndex& ix, int64_t T, int64_t Q);
+
+// The large-k list path (bm25mi_large.hip) for kMaxK < k <= kLargeListMaxK:
+// large_geom's SAMPLE (P = 0: not applicable), theta, REST into lists, the
+// k-th key of each list, compaction and a row sort; queries the lists cannot
+// serve go through launch_search_large on their own (*n_fallback of them;
+// the path synchronises the stream once to count them).  ws: the handle's
+// workspace (claim counters, counters, segment table).
+constexpr int64_t kLargeListMaxK = 131072;
+SampleGeom large_geom(const DevIndex& ix, int64_t k);
+hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
+                                     int64_t T, int k, const Workspace& ws, int32_t* d_docs,
+                                     float* d_scores, int64_t* n_fallback, hipStream_t stream);
+
 // W lists [Q, k] (docs and scores at element w * rank_stride) -> the best k
 // of each query by (score desc, doc asc), for any k (a segmented sort of the
 // W k keys of each query).  Padding (doc -1, score bits ~0) sorts last.

@@ -2870,6 +2870,7 @@ static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t T, int64_
     if constexpr (PH == kSample) {  // m keys per sample tile: a build per m
       if (sg.M == 2) return launch_flat_tl<S, PH, 2>(ix, q, T, Qb, sg, ws, st);
       if (sg.M == kTileM) return launch_flat_tl<S, PH, kTileM>(ix, q, T, Qb, sg, ws, st);
+      if (sg.M == kLargeM) return launch_flat_tl<S, PH, kLargeM>(ix, q, T, Qb, sg, ws, st);
     }
     return launch_flat_tl<S, PH, 1>(ix, q, T, Qb, sg, ws, st);
   }
@@ -3074,6 +3075,48 @@ hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q
   BM25_SHIFT_DISPATCH(CALL)
 #undef CALL
   return hipGetLastError();
+}
+
+// The large-k list path's score passes (bm25mi_large.hip): a SAMPLE pass with
+// kLargeM keys per sample tile (the best of each 256-doc slice) into
+// keys[Q][g.S], then a REST pass that appends every key >= ws.theta[q] to
+// ws.list (capacity ws.list_cap, counts ws.list_cnt: the caller's buffers).
+hipError_t launch_sample_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                               const SampleGeom& g, uint64_t* keys, const Workspace& ws,
+                               hipStream_t stream) {
+  if (Q == 0 || ix.ntiles == 0) return hipSuccess;
+  if (g.m != kLargeM || g.P < 2 || !use_flat(ix, T, Q)) return hipErrorInvalidValue;
+  if (sample_count(ix.ntiles, g.P, g.G) * g.m < g.S)
+    hipMemsetAsync(keys, 0, sizeof(uint64_t) * Q * g.S, stream);
+  if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, d_queries, Q, T, ws, stream);
+  Stage sg = main_stage(ix, Q, g.P, ws);
+  sg.ctr_region = 0;
+  sg.M = g.m;
+  sg.G = g.G;
+  sg.cand_out = keys;
+  sg.cstride = g.S;
+#define CALL(s_) launch_phase<s_, kSample>(ix, d_queries, T, Q, sg, ws, stream)
+  BM25_SHIFT_DISPATCH(CALL)
+#undef CALL
+  return hipGetLastError();
+}
+
+hipError_t launch_rest_lists(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
+                             const SampleGeom& g, const Workspace& ws, hipStream_t stream) {
+  if (Q == 0 || ix.ntiles == 0) return hipSuccess;
+  if (!use_flat(ix, T, Q)) return hipErrorInvalidValue;
+  Stage sg = main_stage(ix, Q, g.P, ws);
+  sg.ctr_region = 1;
+  sg.M = g.m;
+  sg.G = g.G;
+#define CALL(s_) launch_phase<s_, kRest>(ix, d_queries, T, Q, sg, ws, stream)
+  BM25_SHIFT_DISPATCH(CALL)
+#undef CALL
+  return hipGetLastError();
+}
+
+bool large_list_supported(const DevIndex& ix, int64_t T, int64_t Q) {
+  return ix.nonneg && use_flat(ix, T, Q);
 }
 
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,

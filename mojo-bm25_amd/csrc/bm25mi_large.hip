@@ -387,6 +387,284 @@ hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int
   return hipSuccess;
 }
 
+namespace {
+
+// ---------------------------------------------------------------------------
+// The list path (k in (kMaxK, kLargeListMaxK]): no dense score rows.  A
+// SAMPLE pass keeps the best key of each 256-doc slice of every P-th tile
+// group (launch_sample_large); theta = the k-th best of those keys — k real
+// documents score at least theta, so it is a lower bound of the k-th key;
+// the REST pass appends every key >= theta to the query's list
+// (launch_rest_lists); the k-th key of the list by radix selection, the k
+// keys >= it compacted, the rows sorted (bm25mi_sort.hip) and written.  A
+// query whose list overflowed, or whose sample or list holds fewer than k
+// keys (zero-fill), is answered by the dense path above, on its own.
+// ---------------------------------------------------------------------------
+constexpr int kSelT = 256;
+
+// Wave-aggregated LDS histogram add (a wave's keys that share a digit add once).
+__device__ __forceinline__ void hist_add(uint32_t* h, uint32_t d, bool valid) {
+  uint64_t m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const uint64_t bb = __ballot(((d >> b) & 1u) != 0u);
+    m &= ((d >> b) & 1u) ? bb : ~bb;
+  }
+  const uint32_t below =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (valid && below == 0u) atomicAdd(&h[d], (uint32_t)__popcll(m));
+}
+
+// Exclusive scan of one value per thread of a 256-thread workgroup.
+__device__ __forceinline__ uint32_t block_excl256(uint32_t x, uint32_t* wsum) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t incl = wave_scan(x);
+  if (lane == 63u) wsum[w] = incl;
+  __syncthreads();
+  uint32_t pre = 0u;
+  for (uint32_t j = 0; j < w; ++j) pre += wsum[j];
+  __syncthreads();
+  return pre + incl - x;
+}
+
+// The k-th largest non-zero key of each row (one workgroup per row), 8 bits
+// per pass from the top; a row decided early (every key of its prefix is
+// needed) ends with the prefix (lower bits 0), which selects the same keys.
+//   MODE 0 (threshold from the sample keys, rows of `stride` keys): out =
+//     theta moved into the index's doc frame (sample keys carry global ids),
+//     or, with fewer than k keys, a threshold no key reaches and fb = 1;
+//     lens[row] = 0 (the list count the REST pass appends to).
+//   MODE 1 (list select, rows of lens[row] <= cap keys): out = the k-th key;
+//     fb |= 1 when the list overflowed or holds fewer than k keys.
+template <int MODE>
+__global__ __launch_bounds__(kSelT) void row_kth_kernel(const uint64_t* __restrict__ keys,
+                                                        int64_t stride, int32_t* __restrict__ lens,
+                                                        int32_t cap, uint32_t k, int64_t doc_offset,
+                                                        uint64_t* __restrict__ out,
+                                                        int32_t* __restrict__ fb) {
+  __shared__ uint32_t h[256];
+  __shared__ uint32_t wsum[4];
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_need, s_state;  // s_state: 0 continue, 1 decided, 2 too few keys
+  const int64_t row = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  int64_t n = stride;
+  bool over = false;
+  if (MODE == 1) {
+    const int32_t c = lens[row];
+    over = c > cap;
+    n = over ? 0 : c;
+  }
+  const uint64_t* r = keys + row * stride;
+  uint64_t prefix = 0ull;
+  uint32_t need = k;
+  bool found = !over;
+  for (int shift = 56; found && shift >= 0; shift -= 8) {
+    h[t] = 0u;
+    if (t == 0) s_state = 2u;
+    __syncthreads();
+    const int hs = shift + 8;
+    const int64_t rounds = (n + kSelT - 1) / kSelT;  // every lane runs every round (ballots)
+    for (int64_t i0 = 0; i0 < rounds; ++i0) {
+      const int64_t i = i0 * kSelT + t;
+      const uint64_t key = i < n ? r[i] : 0ull;
+      const bool in = key != 0ull && (hs >= 64 || ((key ^ prefix) >> hs) == 0ull);
+      hist_add(h, (uint32_t)(key >> shift) & 255u, in);
+    }
+    __syncthreads();
+    const uint32_t x = h[255 - t];  // thread t: digit 255 - t (from the top)
+    const uint32_t above = block_excl256(x, wsum);
+    if (above < need && need <= above + x) {
+      s_prefix = prefix | ((uint64_t)(255 - t) << shift);
+      s_need = need - above;
+      s_state = (x == need - above || shift == 0) ? 1u : 0u;
+    }
+    __syncthreads();
+    const uint32_t st = s_state;
+    if (st == 2u) {
+      found = false;
+      break;
+    }
+    prefix = s_prefix;
+    need = s_need;
+    __syncthreads();
+    if (st == 1u) break;
+  }
+  if (t != 0) return;
+  if (MODE == 0) {
+    lens[row] = 0;
+    if (found) {  // into the index's frame: tie doc global -> local (a key of this shard)
+      const uint64_t lo = (prefix & 0xFFFFFFFFull) + (uint64_t)doc_offset;
+      out[row] = lo <= 0xFFFFFFFFull ? (prefix & ~0xFFFFFFFFull) | lo
+                                     : ((prefix >> 32) + 1ull) << 32;
+    } else {
+      out[row] = (uint64_t)score_key(__builtin_inff()) << 32;  // no REST key reaches it
+    }
+    fb[row] = found ? 0 : 1;
+  } else {
+    out[row] = found ? prefix : 0ull;
+    if (!found) fb[row] = 1;
+  }
+}
+
+// The k keys >= kth[row] of each list row (exactly k: keys are unique),
+// appended in any order to out[row][0..k); fallback rows are skipped.
+__global__ __launch_bounds__(kSelT) void list_compact_kernel(const uint64_t* __restrict__ list,
+                                                             int64_t C,
+                                                             const int32_t* __restrict__ lens,
+                                                             const uint64_t* __restrict__ kth,
+                                                             const int32_t* __restrict__ fb,
+                                                             int64_t k, uint64_t* __restrict__ out) {
+  __shared__ int32_t s_pos;
+  const int64_t row = blockIdx.x;
+  if (fb[row]) return;  // block-uniform; before the barrier
+  if (threadIdx.x == 0) s_pos = 0;
+  __syncthreads();
+  const uint64_t th = kth[row];
+  const int64_t n = lens[row];
+  const uint64_t* r = list + row * C;
+  const uint32_t lane = threadIdx.x & 63u;
+  const int64_t rounds = (n + kSelT - 1) / kSelT;
+  for (int64_t i0 = 0; i0 < rounds; ++i0) {
+    const int64_t i = i0 * kSelT + threadIdx.x;
+    const uint64_t key = i < n ? r[i] : 0ull;
+    const bool keep = key != 0ull && key >= th;
+    const uint64_t m = __ballot(keep);
+    if (m == 0ull) continue;
+    int p0 = 0;
+    if (lane == 0) p0 = atomicAdd(&s_pos, (int)__popcll(m));
+    p0 = __shfl(p0, 0, 64);
+    const int pos = p0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (keep && pos < k) out[row * k + pos] = key;
+  }
+}
+
+// Rows of the fallback queries: ids[j] = the j-th row with fb set (host-built),
+// queries gathered / results scattered.
+__global__ __launch_bounds__(256) void gather_rows_kernel(const int32_t* __restrict__ src,
+                                                          const int32_t* __restrict__ ids,
+                                                          int64_t n, int64_t width,
+                                                          int32_t* __restrict__ dst) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n * width;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t j = e / width, c = e - j * width;
+    dst[e] = src[(int64_t)ids[j] * width + c];
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const int32_t* __restrict__ sd,
+                                                           const float* __restrict__ ss,
+                                                           const int32_t* __restrict__ ids,
+                                                           int64_t n, int64_t width,
+                                                           int32_t* __restrict__ dd,
+                                                           float* __restrict__ ds) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n * width;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t j = e / width, c = e - j * width;
+    dd[(int64_t)ids[j] * width + c] = sd[e];
+    ds[(int64_t)ids[j] * width + c] = ss[e];
+  }
+}
+
+}  // namespace
+
+// Geometry of the list path: sampling stride P (the largest of 8, 4, 2 whose
+// sample holds >= 2k keys, else 2 when it holds >= k), kLargeM keys per
+// sample tile; P = 0: the list path does not apply.
+SampleGeom large_geom(const DevIndex& ix, int64_t k) {
+  for (int need = 2; need >= 1; --need)
+    for (int P = 8; P >= 2; P >>= 1) {
+      if (ix.ntiles < 2 * P) continue;
+      const int G = ix.ntiles >= 4 * kSampleGroup * P ? kSampleGroup : 1;
+      // sample_count (bm25mi_kernels.hip): groups of G tiles every G * P
+      const int64_t r = ix.ntiles % (G * P);
+      const int64_t nS = (ix.ntiles / (G * P)) * G + (r < G ? r : G);
+      if (nS * kLargeM >= need * k && (need == 2 || P == 2)) return SampleGeom{P, kLargeM, nS * kLargeM, G};
+    }
+  return SampleGeom{0, 0, 0, 1};
+}
+
+hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
+                                     int64_t T, int k, const Workspace& ws, int32_t* d_docs,
+                                     float* d_scores, int64_t* n_fallback, hipStream_t st) {
+  *n_fallback = 0;
+  if (Q == 0 || k == 0) return hipSuccess;
+  const SampleGeom g = large_geom(ix, k);
+  if (g.P == 0 || k > ix.n_docs || !large_list_supported(ix, T, Q)) return hipErrorInvalidValue;
+  ix.disp.kernels |= kKLarge | kKFlatSample | kKFlatRest;
+  ix.disp.sample_p = g.P;
+  const int64_t C = std::min<int64_t>(1 << 20, 4 * (int64_t)g.P * k);  // list capacity
+  const int64_t per_q = (g.S + C + 2 * (int64_t)k) * 8 + 64 + 8 * (int64_t)k +
+                        (int64_t)radix_sort_scratch_bytes(k) + 64;
+  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));
+  G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / C - 1));
+  Scratch sc(st);
+  uint64_t *skeys = nullptr, *theta = nullptr, *list = nullptr, *kth = nullptr, *keys = nullptr,
+           *alt = nullptr;
+  int32_t *cnt = nullptr, *fb = nullptr;
+  char* tmp = nullptr;
+  LK_TRY(sc.get(&skeys, G * g.S));
+  LK_TRY(sc.get(&theta, G));
+  LK_TRY(sc.get(&list, G * C));
+  LK_TRY(sc.get(&kth, G));
+  LK_TRY(sc.get(&keys, G * k));
+  LK_TRY(sc.get(&alt, G * k));
+  LK_TRY(sc.get(&cnt, G));
+  LK_TRY(sc.get(&fb, Q));
+  LK_TRY(sc.get(&tmp, sort_bytes(G, k)));
+  Workspace w = ws;  // the handle's claim counters, counters and segment table
+  w.theta = theta;
+  w.list = list;
+  w.list_cnt = cnt;
+  w.list_cap = (int32_t)C;
+  for (int64_t q0 = 0; q0 < Q; q0 += G) {
+    const int64_t gq = std::min<int64_t>(G, Q - q0);
+    const int32_t* q = d_queries + q0 * T;
+    LK_TRY(launch_sample_large(ix, q, gq, T, g, skeys, w, st));
+    hipLaunchKernelGGL(row_kth_kernel<0>, dim3((unsigned)gq), dim3(kSelT), 0, st, skeys, g.S, cnt,
+                       0, (uint32_t)k, ix.doc_offset, theta, fb + q0);
+    LK_TRY(hipMemsetAsync(ws.counters, 0, sizeof(int32_t) * kCounters, st));
+    LK_TRY(launch_rest_lists(ix, q, gq, T, g, w, st));
+    hipLaunchKernelGGL(row_kth_kernel<1>, dim3((unsigned)gq), dim3(kSelT), 0, st, list, C, cnt,
+                       (int32_t)C, (uint32_t)k, 0ll, kth, fb + q0);
+    hipLaunchKernelGGL(list_compact_kernel, dim3((unsigned)gq), dim3(kSelT), 0, st, list, C, cnt,
+                       kth, fb + q0, (int64_t)k, keys);
+    const uint64_t* sorted = nullptr;
+    LK_TRY(sort_rows(keys, alt, gq, k, tmp, &sorted, st));
+    hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(gq * k, 256, 4096)), dim3(256), 0, st, sorted,
+                       (int64_t)k, gq, k, k, ix.doc_offset, d_docs + q0 * k, d_scores + q0 * k);
+    LK_TRY(hipGetLastError());
+  }
+  // the queries the lists could not serve: the dense path, on their own (the
+  // one host synchronisation of this path: their number sizes that pass)
+  std::vector<int32_t> hfb((size_t)Q);
+  LK_TRY(hipMemcpyAsync(hfb.data(), fb, sizeof(int32_t) * Q, hipMemcpyDeviceToHost, st));
+  LK_TRY(hipStreamSynchronize(st));
+  std::vector<int32_t> ids;
+  for (int64_t i = 0; i < Q; ++i)
+    if (hfb[(size_t)i]) ids.push_back((int32_t)i);
+  *n_fallback = (int64_t)ids.size();
+  if (ids.empty()) return hipSuccess;
+  const int64_t nf = (int64_t)ids.size();
+  int32_t *d_ids = nullptr, *fq = nullptr, *fd = nullptr;
+  float* fs = nullptr;
+  LK_TRY(sc.get(&d_ids, nf));
+  LK_TRY(sc.get(&fq, nf * std::max<int64_t>(T, 1)));
+  LK_TRY(sc.get(&fd, nf * k));
+  LK_TRY(sc.get(&fs, nf * k));
+  LK_TRY(hipMemcpyAsync(d_ids, ids.data(), sizeof(int32_t) * nf, hipMemcpyHostToDevice, st));
+  if (T > 0)
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(nf * T, 256, 4096)), dim3(256), 0, st,
+                       d_queries, d_ids, nf, T, fq);
+  LK_TRY(launch_search_large(ix, fq, nf, T, k, fd, fs, st));
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for(nf * k, 256, 4096)), dim3(256), 0, st, fd,
+                     fs, d_ids, nf, (int64_t)k, d_docs, d_scores);
+  // (ids lives on the host until the copy above has run)
+  LK_TRY(hipStreamSynchronize(st));
+  return hipGetLastError();
+}
+
 hipError_t launch_merge_large(const int32_t* d_docs, const float* d_scores, int64_t W, int64_t Q,
                               int k, int64_t rank_stride, int32_t* d_out_docs,
                               float* d_out_scores, hipStream_t st) {

@@ -176,3 +176,33 @@ def test_large_merge_random_lists(gpu):
         order = np.lexsort((d[ok], -s[ok].astype(np.float64)))[:k]
         assert np.array_equal(md.cpu().numpy()[qi], d[ok][order])
         assert np.array_equal(ms.cpu().numpy()[qi].view(np.uint32), s[ok][order].view(np.uint32))
+
+
+@pytest.mark.parametrize("segments", ["dense", "sparse"])
+def test_large_k_list_path(gpu, segments):
+    """k > 4096 without dense score rows — a SAMPLE pass
+    with the best key of every 256-doc slice of the sample tiles, theta = its
+    k-th key, the REST pass listing every key >= theta, the k-th key of each
+    list, compaction and the hand-written row sort.  Bit-exact vs the oracle;
+    rows the lists cannot serve (all padding, rare terms: fewer than k keys)
+    go to the dense rows on their own; large_lists = 0 gives the same bits."""
+    from bm25mi import synth
+    cfg = synth.Config("L", 3_000_000, 20_000, 40_000_000, 48, 8, 5000)
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    q[0, :] = -1                                   # all padding
+    q[1, 1:] = q[1, 0]                             # one term eight times
+    q[2, :] = np.argsort(np.diff(ip))[:8]          # rare terms: fewer than k docs
+    index = _idx(ip, ix, dt, cfg.n_docs, segments=segments)
+    for k in (4097, 7000):
+        ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, k, threads=8)
+        index.set_option("large_lists", 1)
+        _exact(index.search(q, k), ref)
+        d = index.last_dispatch()
+        assert {"large_k", "flat_sample", "flat_rest"} <= d["kernels"] and d["sample_p"] >= 2, d
+        dense = index.search_stats()["large_dense_queries"]
+        assert 2 <= dense <= 8, dense           # rows 0 and 2 (and few others)
+        index.set_option("large_lists", 0)
+        _exact(index.search(q, k), ref)
+        assert index.search_stats()["large_dense_queries"] == -1
+    index.close()

@@ -1206,10 +1206,16 @@ def test_tile_bound_skips_exact(gpu, T):
         st = index.search_stats()
         skipped = st["bound_skipped_tiles"]
         assert skipped > 0, skipped
-        # the postings of the skipped pairs (bench.py's roofline.bound_skip)
+        # the postings of the skipped pairs (bench.py's roofline.bound_skip): the
+        # all-padding row skips every tile with no posting in it; at k = 10
+        # (tile-bound theta) the other rows skip tiles of their common terms too
         df = np.diff(ip)
         per_query = sum(int(df[np.unique(r[r >= 0])].sum()) for r in q)
-        assert 0 < st["bound_skipped_postings"] < per_query, (st, per_query)
+        ntiles = index.info()["n_tiles"]
+        assert 0 <= st["bound_skipped_postings"] < per_query, (st, per_query)
+        assert (st["bound_skipped_postings"] > 0) == (skipped > ntiles), (st, ntiles)
+        if k == 10:
+            assert skipped > ntiles, st
         index.set_option("tile_bound", 0)
         _exact(index.search(q, k), ref)
         st = index.search_stats()
