@@ -792,6 +792,14 @@ constexpr int kQW = 4;
 #define BM25_CLAMP 0
 #endif
 
+#ifndef BM25_TRACE  // dev variant builds: per-wave start / end clocks of the REST pass
+#define BM25_TRACE 0
+#endif
+#if BM25_TRACE
+constexpr int kTraceWaves = 1 << 14;
+__device__ uint64_t g_bm25_trace[4 * kTraceWaves];  // (start, end, items, rows) per wave
+#endif
+
 // Inclusive prefix sum over the wave (DPP: rows of 16, then the row carries).
 __device__ __forceinline__ uint32_t scan64(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
@@ -934,6 +942,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     }
   };
   const PostingRsrc pr = posting_rsrc(a);
+#if BM25_TRACE
+  const uint64_t tr_t0 = wall_clock64();
+  uint32_t tr_items = 0, tr_rows = 0;
+#endif
   const uint32_t lt = lane & (TT - 1u), li = lane >> TL;  // segment lane: tile li, term lt
   const int64_t nbp = (a.ntiles + 7) >> 3;                // 8-tile groups of the sparse seg rows
 
@@ -1036,6 +1048,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   int32_t tmN2 = 0;
   // enter item nx (descriptors dN) on the issue side; advance the prefetch
   auto enter_item = [&]() {
+#if BM25_TRACE
+    ++tr_items;
+#endif
     const bool th_pos = PH == kRest && th_positive(thN);
     const uint32_t t32 = (uint32_t)(nx.b * BW) + li;  // REST: phase tile = tile
     const bool smp = skipping && ((t32 >> lgG) & (uint32_t)(P - 1)) == 0u;
@@ -1277,7 +1292,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   while (!done) {
 #pragma unroll
     for (int s = 0; s < kFR; ++s) step(s);
+#if BM25_TRACE
+    tr_rows += kFR;
+#endif
   }
+#if BM25_TRACE
+  if (PH == kRest && lane == 0 && blockIdx.x < kTraceWaves) {
+    uint64_t* tr = g_bm25_trace + 4 * blockIdx.x;
+    tr[0] = tr_t0;
+    tr[1] = wall_clock64();
+    tr[2] = tr_items;
+    tr[3] = tr_rows;
+  }
+#endif
   if (curTi != kNoTile) epilogue();
   if (PH == kRest && stats != nullptr) {  // bound-skipped tiles (and postings) of this wave
     const uint32_t nb = wave_sum_u32(nbound);
@@ -3248,3 +3275,13 @@ hipError_t launch_merge_lists(const int32_t* d_docs, const float* d_scores, int6
 }
 
 }  // namespace bm25mi
+
+#if BM25_TRACE
+// Dev variant builds only: the last REST pass's per-wave trace (4 u64 per
+// wave: start clock, end clock, items, rows; 100 MHz clock).
+extern "C" int bm25_debug_trace(uint64_t* out, int64_t n_waves) {
+  const int64_t n = n_waves < bm25mi::kTraceWaves ? n_waves : bm25mi::kTraceWaves;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(bm25mi::g_bm25_trace), sizeof(uint64_t) * 4 * n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+}
+#endif

@@ -28,6 +28,8 @@
 // zero-score (untouched) documents fill a row the same way.
 #include "bm25mi_internal.h"
 
+#include <cfloat>
+
 #include <algorithm>
 #include <vector>
 
@@ -432,10 +434,13 @@ __device__ __forceinline__ uint32_t block_excl256(uint32_t x, uint32_t* wsum) {
 // needed) ends with the prefix (lower bits 0), which selects the same keys.
 //   MODE 0 (threshold from the sample keys, rows of `stride` keys): out =
 //     theta moved into the index's doc frame (sample keys carry global ids),
-//     or, with fewer than k keys, a threshold no key reaches and fb = 1;
-//     lens[row] = 0 (the list count the REST pass appends to).
-//   MODE 1 (list select, rows of lens[row] <= cap keys): out = the k-th key;
-//     fb |= 1 when the list overflowed or holds fewer than k keys.
+//     or, with fewer than k keys, the zero-fill threshold (every positive
+//     document is listed); lens[row] = 0 (the list count the REST pass
+//     appends to); fb[row] = 0.
+//   MODE 1 (list select, rows of lens[row] <= cap keys): out = the k-th key,
+//     or 0 when the list holds fewer than k keys (all of them, then the
+//     smallest zero-score documents: list_compact_kernel); fb = 1 when the
+//     list overflowed.
 template <int MODE>
 __global__ __launch_bounds__(kSelT) void row_kth_kernel(const uint64_t* __restrict__ keys,
                                                         int64_t stride, int32_t* __restrict__ lens,
@@ -498,17 +503,23 @@ __global__ __launch_bounds__(kSelT) void row_kth_kernel(const uint64_t* __restri
       out[row] = lo <= 0xFFFFFFFFull ? (prefix & ~0xFFFFFFFFull) | lo
                                      : ((prefix >> 32) + 1ull) << 32;
     } else {
-      out[row] = (uint64_t)score_key(__builtin_inff()) << 32;  // no REST key reaches it
+      out[row] = (uint64_t)score_key(FLT_MIN) << 32;  // every positive doc (zero fill)
     }
-    fb[row] = found ? 0 : 1;
+    fb[row] = 0;
   } else {
     out[row] = found ? prefix : 0ull;
-    if (!found) fb[row] = 1;
+    if (over) fb[row] = 1;
   }
 }
 
 // The k keys >= kth[row] of each list row (exactly k: keys are unique),
-// appended in any order to out[row][0..k); fallback rows are skipped.
+// appended in any order to out[row][0..k); fallback rows are skipped.  A
+// row of fewer than k keys (kth = 0: its query has fewer than k positive
+// documents) takes all of them and then the smallest document ids it does
+// not hold, at score 0 (the reference's argpartition fills its top-k with
+// zero-score documents; the (score desc, doc asc) order takes the smallest):
+// an LDS bitmap of the held ids below k, scanned in order.
+constexpr int kZeroFillWords = (int)(kLargeListMaxK / 32);
 __global__ __launch_bounds__(kSelT) void list_compact_kernel(const uint64_t* __restrict__ list,
                                                              int64_t C,
                                                              const int32_t* __restrict__ lens,
@@ -516,12 +527,55 @@ __global__ __launch_bounds__(kSelT) void list_compact_kernel(const uint64_t* __r
                                                              const int32_t* __restrict__ fb,
                                                              int64_t k, uint64_t* __restrict__ out) {
   __shared__ int32_t s_pos;
+  __shared__ uint32_t bm[kZeroFillWords];
+  __shared__ uint32_t wsum[4];
   const int64_t row = blockIdx.x;
-  if (fb[row]) return;  // block-uniform; before the barrier
-  if (threadIdx.x == 0) s_pos = 0;
-  __syncthreads();
+  if (fb[row]) return;  // block-uniform; before the barriers
   const uint64_t th = kth[row];
   const int64_t n = lens[row];
+  if (th == 0ull) {  // zero fill: all n < k keys, then the first k - n ids not held
+    const uint64_t* r = list + row * C;
+    const int64_t words = (k + 31) >> 5;
+    for (int64_t w = threadIdx.x; w < words; w += kSelT) bm[w] = 0u;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < n; i += kSelT) {
+      const uint64_t key = r[i];
+      out[row * k + i] = key;
+      const uint32_t d = 0xFFFFFFFFu - (uint32_t)key;
+      if ((int64_t)d < k) atomicOr(&bm[d >> 5], 1u << (d & 31u));
+    }
+    __syncthreads();
+    const uint64_t zkey = (uint64_t)score_key(0.f) << 32;
+    uint32_t carry = 0u;
+    for (int64_t w0 = 0; w0 < words; w0 += kSelT) {
+      const int64_t w = w0 + threadIdx.x;
+      uint32_t free_bits = 0u;
+      if (w < words) {
+        free_bits = ~bm[w];
+        const int64_t hi = k - 32 * w;  // ids past k - 1 are not candidates
+        if (hi < 32) free_bits &= (1u << hi) - 1u;
+      }
+      const uint32_t c = (uint32_t)__popc(free_bits);
+      const uint32_t ex = block_excl256(c, wsum);
+      uint32_t pos = carry + ex;
+      while (free_bits != 0u && (int64_t)(n + pos) < k) {
+        const uint32_t b = (uint32_t)__builtin_ctz(free_bits);
+        free_bits &= free_bits - 1u;
+        const uint32_t d = (uint32_t)(32 * w) + b;
+        out[row * k + n + pos] = zkey | (uint64_t)(0xFFFFFFFFu - d);
+        ++pos;
+      }
+      // every thread needs the round's total: the last thread's ex + c
+      __shared__ uint32_t s_tot;
+      if (threadIdx.x == kSelT - 1) s_tot = ex + c;
+      __syncthreads();
+      carry += s_tot;
+      __syncthreads();
+    }
+    return;
+  }
+  if (threadIdx.x == 0) s_pos = 0;
+  __syncthreads();
   const uint64_t* r = list + row * C;
   const uint32_t lane = threadIdx.x & 63u;
   const int64_t rounds = (n + kSelT - 1) / kSelT;
@@ -594,7 +648,10 @@ hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_querie
   if (g.P == 0 || k > ix.n_docs || !large_list_supported(ix, T, Q)) return hipErrorInvalidValue;
   ix.disp.kernels |= kKLarge | kKFlatSample | kKFlatRest;
   ix.disp.sample_p = g.P;
-  const int64_t C = std::min<int64_t>(1 << 20, 4 * (int64_t)g.P * k);  // list capacity
+  // list capacity: the list_cap option, else 4 P k (the k-th sample key of a
+  // 1-in-P sample sits near the (P k)-th key; 4x headroom for slice effects)
+  const int64_t C = ix.opt.list_cap > 0 ? (int64_t)ix.opt.list_cap
+                                        : std::min<int64_t>(1 << 20, 4 * (int64_t)g.P * k);
   const int64_t per_q = (g.S + C + 2 * (int64_t)k) * 8 + 64 + 8 * (int64_t)k +
                         (int64_t)radix_sort_scratch_bytes(k) + 64;
   int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));

@@ -23,6 +23,18 @@ for step in ${STEPS:-tests lines}; do
     timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -20 $OUT/bench.err; exit 1; }
     cat $OUT/bench.json
     ;;
+  k10000)  # the large-k side line
+    timeout -k 10 300 python -u bench.py --k 10000 --steps 5 --warmup 2 --cpu-queries 0 --e2e-batches 0 > $OUT/bench_k10000.json 2> $OUT/bench_k10000.err || { echo bench k10000 failed; tail -20 $OUT/bench_k10000.err; exit 1; }
+    cat $OUT/bench_k10000.json
+    ;;
+  side)  # the threshold side lines: uniform weights (default options, and theta_bound 0), lucene-scored
+    timeout -k 10 400 python -u bench.py --config c3u --cpu-queries 0 --e2e-batches 0 > $OUT/bench_c3u.json 2> $OUT/bench_c3u.err || { echo bench c3u failed; tail -20 $OUT/bench_c3u.err; exit 1; }
+    cat $OUT/bench_c3u.json
+    BM25_THETA_BOUND=0 timeout -k 10 400 python -u bench.py --config c3u --cpu-queries 0 --e2e-batches 0 > $OUT/bench_c3u_tb0.json 2> $OUT/bench_c3u_tb0.err || { echo bench c3u tb0 failed; tail -20 $OUT/bench_c3u_tb0.err; exit 1; }
+    cat $OUT/bench_c3u_tb0.json
+    timeout -k 10 500 python -u bench.py --config c3l --cpu-queries 0 --e2e-batches 0 > $OUT/bench_c3l.json 2> $OUT/bench_c3l.err || { echo bench c3l failed; tail -20 $OUT/bench_c3l.err; exit 1; }
+    cat $OUT/bench_c3l.json
+    ;;
   lines)
     timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -20 $OUT/bench.err; exit 1; }
     cat $OUT/bench.json

@@ -194,15 +194,51 @@ def test_large_k_list_path(gpu, segments):
     q[1, 1:] = q[1, 0]                             # one term eight times
     q[2, :] = np.argsort(np.diff(ip))[:8]          # rare terms: fewer than k docs
     index = _idx(ip, ix, dt, cfg.n_docs, segments=segments)
-    for k in (4097, 7000):
+    # 1465 tiles: the sample of every other tile group holds 5888 slice keys —
+    # the list path serves k <= 5888; k = 7000 takes the dense rows
+    for k, lists in ((4097, True), (5500, True), (7000, False)):
         ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, k, threads=8)
         index.set_option("large_lists", 1)
         _exact(index.search(q, k), ref)
         d = index.last_dispatch()
-        assert {"large_k", "flat_sample", "flat_rest"} <= d["kernels"] and d["sample_p"] >= 2, d
-        dense = index.search_stats()["large_dense_queries"]
-        assert 2 <= dense <= 8, dense           # rows 0 and 2 (and few others)
+        if lists:
+            assert {"large_k", "flat_sample", "flat_rest"} <= d["kernels"], d
+            assert d["sample_p"] >= 2, d
+            # zero-fill rows (padding, rare terms) are completed in the lists too
+            assert index.search_stats()["large_dense_queries"] == 0
+        else:
+            assert d["kernels"] == {"large_k"}, d
+            assert index.search_stats()["large_dense_queries"] == -1
         index.set_option("large_lists", 0)
         _exact(index.search(q, k), ref)
         assert index.search_stats()["large_dense_queries"] == -1
+    index.close()
+
+
+def test_large_k_list_path_overflow_falls_back(gpu):
+    """A list longer than its capacity goes to the dense rows, for that query
+    alone: one term covering every document with uniform scores lists ~15k
+    keys above the sampled threshold at k = 4200 (capacity forced to 6000 by
+    the list_cap option); the other queries stay on the lists.  Bit-exact."""
+    rng = np.random.default_rng(12)
+    N, V = 3_000_000, 60
+    indptr, idx, dat = [0], [], []
+    for t in range(V):
+        df = N if t == 0 else int(rng.integers(1000, 40_000))
+        idx.append(np.arange(N, dtype=np.int32) if t == 0 else
+                   np.sort(rng.choice(N, df, replace=False)).astype(np.int32))
+        dat.append(rng.uniform(0.05, 3.0, df).astype(np.float32))
+        indptr.append(indptr[-1] + df)
+    ip, ix, dt = np.array(indptr, np.int64), np.concatenate(idx), np.concatenate(dat)
+    q = rng.integers(1, V, size=(12, 6)).astype(np.int32)
+    q[0, :] = -1
+    q[0, 0] = 0  # every document
+    index = _idx(ip, ix, dt, N)
+    k = 4200
+    ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
+    _exact(index.search(q, k), ref)
+    assert index.search_stats()["large_dense_queries"] == 0
+    index.set_option("list_cap", 6000)
+    _exact(index.search(q, k), ref)
+    assert 1 <= index.search_stats()["large_dense_queries"] < len(q)
     index.close()
