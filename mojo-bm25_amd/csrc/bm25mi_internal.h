@@ -156,6 +156,11 @@ struct Workspace {
                                  // [5] (query, tile) pairs REST skipped by their tile bound,
                                  // [6..7] (a u64) the postings of those pairs
   int32_t* slow = nullptr;       // [Q] those queries
+  // the large-k list path's REST (bm25mi_large.hip sets them on its copy):
+  // per-(query, tile) slots of slot_cap keys and their counts; null otherwise
+  uint64_t* slots = nullptr;
+  int32_t* slot_cnt = nullptr;
+  int32_t slot_cap = 0;
   int32_t* wctr = nullptr;       // [kWctrRegions][kWctrInts] item-claim counters: zeroed once
                                  // at allocation; the last wave of each counter's sharers
                                  // re-zeroes it (and its finished count) at the end of every

@@ -587,6 +587,121 @@ __device__ __forceinline__ void emit_rest(float* acc, int64_t tile, int64_t n_do
   zero_acc<S>(acc);  // (LDS order: after every read above)
 }
 
+// The large-k list path's REST tiles: as emit_rest, but a tile's keys go to
+// its own slot of Cb keys (slot_n: how many it has, possibly more than Cb) at
+// positions counted inside the tile, so the common case takes no atomic — a
+// returning atomic per chunk stalls the wave for the device-scope round trip,
+// and at k = 10 000 most tiles list a few keys.  Keys past the slot go to the
+// query's overflow list (capacity Co, count ovf_cnt: one atomic per such
+// chunk).  slot_pack_kernel (bm25mi_large.hip) gathers slots and overflow
+// into the query's list.
+template <int S>
+__device__ __forceinline__ void emit_rest_slot(float* acc, int64_t tile, int64_t n_docs,
+                                               uint64_t theta, uint64_t* __restrict__ slot,
+                                               int32_t Cb, int32_t* __restrict__ slot_n,
+                                               uint64_t* __restrict__ ovf,
+                                               int32_t* __restrict__ ovf_cnt, int32_t Co) {
+  constexpr int D = 1 << S;
+  float4* a4 = reinterpret_cast<float4*>(acc);
+  const uint32_t lane = lane_id();
+  const float th = key_score((uint32_t)(theta >> 32));
+  const int64_t base = tile << S;
+  const int lim = (int)max<int64_t>(-1, min<int64_t>(D, n_docs - base));
+  const int tie = (int)max<int64_t>(
+      -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base + 1));
+  int32_t n = 0;  // the tile's keys so far (wave-uniform)
+#pragma unroll 1
+  for (int j0 = 0; j0 < D / 256; j0 += 2) {
+    const float4 f0 = a4[j0 * 64 + lane], f1 = a4[(j0 + 1) * 64 + lane];
+    const float fe[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+    const float mx = fmaxf(fmaxf(fmaxf(fe[0], fe[1]), fmaxf(fe[2], fe[3])),
+                           fmaxf(fmaxf(fe[4], fe[5]), fmaxf(fe[6], fe[7])));
+    int c = 0;
+    if (!(mx < th && lim == D)) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int d = (int)entry_doc(4 * j0 + e, lane);
+        c += (d < lim) & ((fe[e] > th) | ((fe[e] == th) & (d < tie)));
+      }
+    }
+    if (__ballot(c > 0) == 0) continue;
+    const uint32_t incl = wave_incl_scan((uint32_t)c);
+    const int32_t tot = (int32_t)__builtin_amdgcn_readlane(incl, 63);
+    int pos = n + (int)incl - c;
+    const int32_t past = max(n, Cb);  // the first position of this chunk beyond the slot
+    int obase = 0;
+    if (n + tot > past) {  // (uniform) rare: the slot is full
+      if (lane == 0) obase = atomicAdd(ovf_cnt, n + tot - past);
+      obase = __shfl(obase, 0, 64) - past;  // overflow index = obase + position
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int d = (int)entry_doc(4 * j0 + e, lane);
+      const bool pass = (d < lim) & ((fe[e] > th) | ((fe[e] == th) & (d < tie)));
+      if (pass) {
+        const uint64_t key = ((uint64_t)score_key(fe[e]) << 32) |
+                             (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + d));
+        if (pos < Cb) slot[pos] = key;
+        else if (obase + pos < Co) ovf[obase + pos] = key;
+        ++pos;
+      }
+    }
+    n += tot;
+  }
+  if (n > 0 && lane == 0) *slot_n = n;
+  zero_acc<S>(acc);  // (LDS order: after every read above)
+}
+
+// The large-k list path's REST tiles with a crossing list: the row loop has
+// recorded (xl, n of them) the slot of every document whose running sum
+// reached theta's score — once per document: sums only grow — so only those
+// are tested and keyed, into the tile's slot as emit_rest_slot does, instead
+// of a pass over the tile's 2048 accumulators.
+constexpr int kCrossCap = 256;  // crossing-list entries per wave (512 B of LDS)
+template <int S>
+__device__ __forceinline__ void emit_cross(float* acc, const uint16_t* xl, int32_t nx,
+                                           int64_t tile, int64_t n_docs, uint64_t theta,
+                                           uint64_t* __restrict__ slot, int32_t Cb,
+                                           int32_t* __restrict__ slot_n,
+                                           uint64_t* __restrict__ ovf,
+                                           int32_t* __restrict__ ovf_cnt, int32_t Co) {
+  constexpr int D = 1 << S;
+  const uint32_t lane = lane_id();
+  const float th = key_score((uint32_t)(theta >> 32));
+  const int64_t base = tile << S;
+  const int lim = (int)max<int64_t>(-1, min<int64_t>(D, n_docs - base));
+  const int tie = (int)max<int64_t>(
+      -1, min<int64_t>(D, (int64_t)(0xFFFFFFFFu - (uint32_t)theta) - base + 1));
+  int32_t n = 0;
+  for (int32_t i0 = 0; i0 < nx; i0 += 64) {
+    const int32_t i = i0 + (int32_t)lane;
+    const uint32_t off = i < nx ? (uint32_t)xl[i] : 0u;
+    const int d = (int)(off >> 2);
+    const float f = acc[d];
+    const bool pass = i < nx && d < lim && ((f > th) | ((f == th) & (d < tie)));
+    const uint64_t m = __ballot(pass);
+    if (m == 0ull) continue;
+    const int32_t tot = (int32_t)__popcll(m);
+    const int pos = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const int32_t past = max(n, Cb);
+    int obase = 0;
+    if (n + tot > past) {  // (uniform) rare: the slot is full
+      if (lane == 0) obase = atomicAdd(ovf_cnt, n + tot - past);
+      obase = __shfl(obase, 0, 64) - past;
+    }
+    if (pass) {
+      const uint64_t key = ((uint64_t)score_key(f) << 32) |
+                           (uint64_t)(0xFFFFFFFFu - (uint32_t)(base + d));
+      if (pos < Cb) slot[pos] = key;
+      else if (obase + pos < Co) ovf[obase + pos] = key;
+    }
+    n += tot;
+  }
+  if (n > 0 && lane == 0) *slot_n = n;
+  zero_acc<S>(acc);  // (LDS order: after every read above)
+}
+
 // Tiles of a phase: SAMPLE visits the sample tiles (sample_tile), ALL and
 // REST every tile.
 template <int PH>
@@ -666,6 +781,38 @@ __device__ __forceinline__ void best_dense(float* acc, int64_t tile, int64_t n_d
     }
     if (lane_id() == 0) out[i] = key;
   }
+}
+
+// M keys per tile on a non-negative index (the flat kernel's SAMPLE epilogue,
+// M > 1): each slice's best sum (a float max: sums >= 0 compare as their bit
+// patterns), keyed with the slice's last document — a key <= its best
+// document's own, so k keys still bound the k-th best from below, as
+// SM == 1's running maximum.  One slice at a time, no second read: a few
+// registers live (best_dense holds 2 M across the tile).
+template <int S, int M>
+__device__ __forceinline__ void best_slices_pos(float* acc, int64_t tile, int64_t n_docs,
+                                                uint32_t idoff, uint64_t* __restrict__ out) {
+  constexpr int per = (1 << S) / 256 / M;  // float4 groups per lane and slice
+  static_assert(per >= 1, "a slice holds at least one float4 per lane");
+  const float4* a4 = reinterpret_cast<const float4*>(acc);
+  const uint32_t lane = lane_id();
+  const int64_t base = tile << S;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    float m = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < per; ++jj) {
+      const float4 f = a4[(i * per + jj) * 64 + lane];
+      m = fmaxf(m, fmaxf(fmaxf(f.x, f.y), fmaxf(f.z, f.w)));
+    }
+    const uint32_t wm = wave_max_u32(__float_as_uint(m));
+    const int64_t last = min<int64_t>(base + (int64_t)(i + 1) * per * 256 - 1, n_docs - 1);
+    const uint64_t key = wm == 0u ? 0ull
+                         : ((uint64_t)score_key(__uint_as_float(wm)) << 32) |
+                               (uint64_t)(0xFFFFFFFFu - (uint32_t)last - idoff);
+    if (lane == (uint32_t)i) out[i] = key;
+  }
+  zero_acc<S>(acc);  // (LDS order: after every read above)
 }
 
 // One key per tile, positive sums only (the flat kernel's SAMPLE epilogue):
@@ -905,12 +1052,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
     int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
     const uint64_t* __restrict__ skeys, int64_t sstride, int32_t BW, uint64_t* mirror,
-    int32_t* __restrict__ stats) {
+    int32_t* __restrict__ stats, int32_t* __restrict__ slot_cnt) {
   constexpr int D = 1 << S;
   constexpr int kFR = PH == kSample ? BM25_FR_S : BM25_FR;  // ring slots (>= 2)
   constexpr uint32_t TT = 1u << TL;                          // term lanes per tile
   constexpr uint32_t kTileMask = (64u >> TL) - 1u;           // tile of a segment lane
   __shared__ __attribute__((aligned(16))) float acc[D + 64];
+  // the large-k list path's REST: the tile's crossing list (emit_cross)
+  constexpr bool kCross = PH == kRest && SM == kLargeM;
+  __shared__ uint16_t xl[kCross ? kCrossCap : 1];
   const uint32_t lane = lane_id();
   // byte offset of this lane's trash slot: it holds -inf, so a masked lane
   // needs no masked score (-inf + any finite score = -inf) and never raises
@@ -1207,17 +1357,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   // sum; REST: the tile holds a key >= theta only if this reaches theta's score)
   float hmax = 0.f;
   bool done = false;
+  // kCross: theta's score for the tile's query, and the tile's crossings
+  // (past kCrossCap, or a threshold that is not positive: the epilogue scans
+  // the whole tile)
+  float thS = 0.f;
+  int32_t ncross = 0;
 
   auto epilogue = [&]() {
     const int32_t ti = ctxE.b * BW + (int32_t)curTi;
     const int64_t tile = tile_of32<PH>((uint32_t)ti, (uint32_t)P, (uint32_t)G);
-    if constexpr (PH == kRest) {
-      const bool flagged = a.nonneg && th_positive(ctxE.th);
-      if (flagged && __ballot(hmax >= key_score((uint32_t)(ctxE.th >> 32))) == 0)
+    if constexpr (kCross) {  // the large-k list path: per-tile slots
+      const int64_t si = (int64_t)ctxE.q * a.ntiles + tile;
+      if (ncross == 0)
         zero_acc<S>(acc);
+      else if (ncross <= kCrossCap)
+        emit_cross<S>(acc, xl, ncross, tile, a.n_docs, ctxE.th, cand + si * cstride,
+                      (int32_t)cstride, slot_cnt + si, list + (int64_t)ctxE.q * C,
+                      list_cnt + ctxE.q, C);
       else
+        emit_rest_slot<S>(acc, tile, a.n_docs, ctxE.th, cand + si * cstride, (int32_t)cstride,
+                          slot_cnt + si, list + (int64_t)ctxE.q * C, list_cnt + ctxE.q, C);
+    } else if constexpr (PH == kRest) {
+      const bool flagged = a.nonneg && th_positive(ctxE.th);
+      if (flagged && __ballot(hmax >= key_score((uint32_t)(ctxE.th >> 32))) == 0) {
+        zero_acc<S>(acc);
+      } else {
         emit_rest<S>(acc, tile, a.n_docs, ctxE.th, list + (int64_t)ctxE.q * C,
                      list_cnt + ctxE.q, C);
+      }
       hmax = 0.f;
     } else if constexpr (PH == kAll) {
       select_top_lds<S>(acc, tile, a.n_docs, kTileM, cand + (int64_t)ctxE.q * cstride + tile * kTileM);
@@ -1241,8 +1408,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
         } else {
           best1_pos<S>(acc, tile, (uint32_t)a.doc_offset, out, mirror ? mirror + (out - cand) : nullptr);
         }
-      } else
+      } else if (SM == kLargeM || a.nonneg) {  // (the large-k list path: non-negative only)
+        best_slices_pos<S, SM>(acc, tile, a.n_docs, (uint32_t)a.doc_offset, out);
+      } else {
         best_dense<S, SM, true>(acc, tile, a.n_docs, (uint32_t)a.doc_offset, out);
+      }
     }
   };
 
@@ -1280,11 +1450,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       // read before the epilogue cleared the accumulator (trash lanes keep -inf)
       xc0 = sc0 == trash ? xc0 : 0.f;
       xc1 = sc1 == trash ? xc1 : 0.f;
+      if constexpr (kCross) {
+        thS = key_score((uint32_t)(ctxE.th >> 32));
+        ncross = th_positive(ctxE.th) ? 0 : kCrossCap + 1;
+      }
     }
     const float y0 = xc0 + ac0, y1 = xc1 + ac1;
     lds_at(sc0) = y0;
     lds_at(sc1) = y1;
-    if (PH == kRest || (PH == kSample && SM == 1)) hmax = fmaxf(hmax, fmaxf(y0, y1));
+    if constexpr (kCross) {  // a doc whose sum reaches theta's score now (trash lanes: -inf)
+      const uint64_t m0 = __ballot((y0 >= thS) & (xc0 < thS));
+      const uint64_t m1 = __ballot((y1 >= thS) & (xc1 < thS));
+      if ((m0 | m1) != 0ull) {
+        const int32_t n0 = (int32_t)__popcll(m0), n1 = (int32_t)__popcll(m1);
+        if (ncross + n0 + n1 <= kCrossCap) {
+          const uint32_t b0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+          const uint32_t b1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+          if ((m0 >> lane) & 1ull) xl[ncross + (int32_t)b0] = (uint16_t)sc0;
+          if ((m1 >> lane) & 1ull) xl[ncross + n0 + (int32_t)b1] = (uint16_t)sc1;
+        }
+        ncross += n0 + n1;
+      }
+    } else if (PH == kRest || (PH == kSample && SM == 1)) {
+      hmax = fmaxf(hmax, fmaxf(y0, y1));
+    }
     done = (wC & kRowDead) != 0u;  // (rows past the last item add nothing)
     prepare((s + 1) % kFR);
   };
@@ -2840,6 +3031,9 @@ template <int S, int PH, int SM, int TL>
 static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t Qb,
                         const Stage& sg, const Workspace& ws, hipStream_t st) {
   int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;
+  // REST of the large-k list path (SM == kLargeM): keys into per-tile slots
+  // (ws.slots, ws.slot_cap keys each, counts ws.slot_cnt), the overflow into ws.list
+  constexpr bool kSlots = PH == kRest && SM == kLargeM;
   // REST skips the sample tiles whose best key is below theta (m = 1 samples
   // in groups of 8 tiles: ws.cand holds this shard's sample keys)
   const bool skip = PH == kRest && sg.sample_keys != nullptr && sg.M == 1 && sg.G == kSampleGroup;
@@ -2865,11 +3059,12 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
     ix.disp.term_lanes = 1 << TL;
     ix.disp.band_tiles[PH] = bw;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, st, a, q, (int32_t)T, sg.P,
-                       sg.G, sg.nq_host, sg.nq_dev, sg.qmap, ws.theta, sg.cand_out, sg.cstride,
+                       sg.G, sg.nq_host, sg.nq_dev, sg.qmap, ws.theta,
+                       kSlots ? ws.slots : sg.cand_out, kSlots ? (int64_t)ws.slot_cap : sg.cstride,
                        ws.list, ws.list_cnt, ws.list_cap, wctr, ix.opt.claim_ch, claim_m,
                        skip ? sg.sample_keys : nullptr, sg.sample_stride, bw,
                        PH == kSample && SM == 1 ? sg.cand_mirror : nullptr,
-                       PH == kRest ? ws.counters + 5 : nullptr);
+                       PH == kRest ? ws.counters + 5 : nullptr, kSlots ? ws.slot_cnt : nullptr);
   };
   if (ix.sparse)
     go(score_flat_kernel<S, PH, SM, true, TL>);
@@ -2899,6 +3094,9 @@ static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t T, int64_
       if (sg.M == kTileM) return launch_flat_tl<S, PH, kTileM>(ix, q, T, Qb, sg, ws, st);
       if (sg.M == kLargeM) return launch_flat_tl<S, PH, kLargeM>(ix, q, T, Qb, sg, ws, st);
     }
+    if constexpr (PH == kRest)  // the large-k list path's slots
+      if (sg.M == kLargeM && ws.slots != nullptr)
+        return launch_flat_tl<S, PH, kLargeM>(ix, q, T, Qb, sg, ws, st);
     return launch_flat_tl<S, PH, 1>(ix, q, T, Qb, sg, ws, st);
   }
   int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;

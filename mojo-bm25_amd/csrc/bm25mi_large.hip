@@ -282,6 +282,103 @@ __global__ __launch_bounds__(256) void lk_write_kernel(const uint64_t* __restric
   }
 }
 
+// Rows of n <= kLdsSortMax keys sorted descending in one workgroup's LDS and
+// written out as lk_write_kernel does (docs + doc_offset and scores; columns
+// n..k-1 and zero keys padded with doc -1 / score bits ~0): a bitonic network
+// over the row padded with zero keys to N = 1024 E, the strides below E inside
+// each thread's E consecutive keys (registers), the others across the LDS.
+// One launch for the sort and the write, and every pass stays on chip: the
+// device-wide radix sort of (row, key) pairs moves 10 passes of 12 B per key
+// through memory.
+constexpr int kLdsSortT = 1024;
+constexpr int kLdsSortMax = 16384;
+
+template <int E>
+__device__ __forceinline__ void bitonic_regs(uint64_t (&r)[E], uint32_t i0, uint32_t size,
+                                             uint32_t j_top) {
+  // the strides j_top, j_top / 2, ..., 1 of merge size `size` (j_top < E)
+#pragma unroll
+  for (uint32_t j = E / 2; j >= 1; j >>= 1) {
+    if (j > j_top) continue;
+#pragma unroll
+    for (uint32_t a = 0; a < (uint32_t)E; ++a) {
+      if (a & j) continue;
+      const bool asc = ((i0 + a) & size) != 0u;
+      const uint64_t x = r[a], y = r[a + j];
+      const bool sw = asc ? (x > y) : (x < y);
+      r[a] = sw ? y : x;
+      r[a + j] = sw ? x : y;
+    }
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(kLdsSortT) void row_sort_write_kernel(
+    const uint64_t* __restrict__ keys, int64_t n, int k, int64_t doc_offset,
+    int32_t* __restrict__ docs, float* __restrict__ scores) {
+  constexpr uint32_t N = (uint32_t)kLdsSortT * E;
+  __shared__ uint64_t buf[N];
+  const int64_t row = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint32_t i0 = t * E;
+  uint64_t r[E];
+  const uint64_t* src = keys + row * n;
+#pragma unroll
+  for (int a = 0; a < E; ++a) r[a] = (int64_t)(i0 + a) < n ? src[i0 + a] : 0ull;
+  for (uint32_t size = 2; size <= (uint32_t)E; size <<= 1) bitonic_regs<E>(r, i0, size, size / 2);
+#pragma unroll
+  for (int a = 0; a < E; ++a) buf[i0 + a] = r[a];
+  __syncthreads();
+  for (uint32_t size = 2 * E; size <= N; size <<= 1) {
+    for (uint32_t j = size / 2; j >= (uint32_t)E; j >>= 1) {
+      const uint32_t lg = (uint32_t)__builtin_ctz(j);
+#pragma unroll
+      for (uint32_t m = 0; m < (uint32_t)E / 2; ++m) {
+        const uint32_t p = t + m * kLdsSortT;                // pair p: i has bit j clear
+        const uint32_t i = ((p >> lg) << (lg + 1)) | (p & (j - 1u));
+        const bool asc = (i & size) != 0u;
+        const uint64_t x = buf[i], y = buf[i + j];
+        if (asc ? (x > y) : (x < y)) {
+          buf[i] = y;
+          buf[i + j] = x;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < E; ++a) r[a] = buf[i0 + a];
+    bitonic_regs<E>(r, i0, size, E / 2);
+#pragma unroll
+    for (int a = 0; a < E; ++a) buf[i0 + a] = r[a];
+    __syncthreads();
+  }
+  for (int64_t i = t; i < k; i += kLdsSortT) {
+    const uint64_t key = i < n ? buf[i] : 0ull;
+    const int64_t e = row * k + i;
+    if (key == 0ull) {
+      docs[e] = -1;
+      scores[e] = __uint_as_float(0xFFFFFFFFu);
+    } else {
+      docs[e] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)key) + doc_offset);
+      scores[e] = key_score((uint32_t)(key >> 32));
+    }
+  }
+}
+
+// Sorts and writes rows [G][n] (n <= kLdsSortMax) into [G][k] results; false
+// when the rows are too long for the LDS sort.
+bool lds_sort_write(const uint64_t* keys, int64_t G, int64_t n, int k, int64_t doc_offset,
+                    int32_t* docs, float* scores, hipStream_t st) {
+  if (n > kLdsSortMax || G <= 0) return false;
+  if (n <= kLdsSortT * 8)
+    hipLaunchKernelGGL(row_sort_write_kernel<8>, dim3((unsigned)G), dim3(kLdsSortT), 0, st, keys, n,
+                       k, doc_offset, docs, scores);
+  else
+    hipLaunchKernelGGL(row_sort_write_kernel<16>, dim3((unsigned)G), dim3(kLdsSortT), 0, st, keys,
+                       n, k, doc_offset, docs, scores);
+  return true;
+}
+
 // Scratch bytes of sorting G rows of n keys (descending): the radix passes'
 // histograms + the row numbers (two buffers).
 int64_t sort_bytes(int64_t G, int64_t n) {
@@ -380,10 +477,13 @@ hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int
     }
     hipLaunchKernelGGL(lk_compact_kernel, grid, dim3(256), 0, st, scores, Np, ix.n_docs, state, cnt,
                        keys, (int64_t)kv);
-    const uint64_t* sorted = nullptr;
-    LK_TRY(sort_rows(keys, alt, g, kv, tmp, &sorted, st));
-    hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(g * k, 256, 4096)), dim3(256), 0, st, sorted,
-                       (int64_t)kv, g, k, kv, ix.doc_offset, d_docs + q0 * k, d_scores + q0 * k);
+    if (!lds_sort_write(keys, g, kv, k, ix.doc_offset, d_docs + q0 * k, d_scores + q0 * k, st)) {
+      const uint64_t* sorted = nullptr;
+      LK_TRY(sort_rows(keys, alt, g, kv, tmp, &sorted, st));
+      hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(g * k, 256, 4096)), dim3(256), 0, st,
+                         sorted, (int64_t)kv, g, k, kv, ix.doc_offset, d_docs + q0 * k,
+                         d_scores + q0 * k);
+    }
     LK_TRY(hipGetLastError());
   }
   return hipSuccess;
@@ -594,6 +694,49 @@ __global__ __launch_bounds__(kSelT) void list_compact_kernel(const uint64_t* __r
   }
 }
 
+// The REST pass's per-tile slots (emit_rest_slot, bm25mi_kernels.hip) of each
+// query gathered into its list: the slots' keys in tile order, then the
+// overflow keys; lens[row] = their number, or cap + 1 when they do not fit
+// (row_kth_kernel<1> then sends the query to the dense path).  One workgroup
+// per query.
+__global__ __launch_bounds__(kSelT) void slot_pack_kernel(const uint64_t* __restrict__ slots,
+                                                          const int32_t* __restrict__ slot_cnt,
+                                                          int64_t ntiles, int32_t Cb,
+                                                          const uint64_t* __restrict__ ovf,
+                                                          int32_t Co, int32_t* __restrict__ lens,
+                                                          uint64_t* __restrict__ list, int64_t C) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t s_tot;
+  const int64_t row = blockIdx.x;
+  const int32_t* cn = slot_cnt + row * ntiles;
+  const uint64_t* sl = slots + row * ntiles * Cb;
+  const int32_t no = lens[row];  // overflow keys (the REST pass's list count)
+  uint64_t* out = list + row * C;
+  if (no > Co) {  // block-uniform, before the barriers
+    if (threadIdx.x == 0) lens[row] = (int32_t)(C + 1);
+    return;
+  }
+  uint32_t carry = 0u;
+  for (int64_t t0 = 0; t0 < ntiles; t0 += kSelT) {
+    const int64_t t = t0 + threadIdx.x;
+    const uint32_t n = t < ntiles ? (uint32_t)min(cn[t], Cb) : 0u;
+    const uint32_t ex = block_excl256(n, wsum);
+    const uint32_t at = carry + ex;
+    for (uint32_t i = 0; i < n; ++i)
+      if ((int64_t)(at + i) < C) out[at + i] = sl[t * Cb + i];
+    if (threadIdx.x == kSelT - 1) s_tot = ex + n;
+    __syncthreads();
+    carry += s_tot;
+    __syncthreads();
+  }
+  for (int32_t i = threadIdx.x; i < no; i += kSelT)
+    if ((int64_t)carry + i < C) out[carry + i] = ovf[row * Co + i];
+  if (threadIdx.x == 0) {
+    const int64_t total = (int64_t)carry + no;
+    lens[row] = total > C ? (int32_t)(C + 1) : (int32_t)total;
+  }
+}
+
 // Rows of the fallback queries: ids[j] = the j-th row with fb set (host-built),
 // queries gathered / results scattered.
 __global__ __launch_bounds__(256) void gather_rows_kernel(const int32_t* __restrict__ src,
@@ -652,15 +795,23 @@ hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_querie
   // 1-in-P sample sits near the (P k)-th key; 4x headroom for slice effects)
   const int64_t C = ix.opt.list_cap > 0 ? (int64_t)ix.opt.list_cap
                                         : std::min<int64_t>(1 << 20, 4 * (int64_t)g.P * k);
-  const int64_t per_q = (g.S + C + 2 * (int64_t)k) * 8 + 64 + 8 * (int64_t)k +
-                        (int64_t)radix_sort_scratch_bytes(k) + 64;
+  // REST's per-tile slots: Cb keys each, ~4x the mean a tile lists when the
+  // list reaches its capacity C; keys past a slot go to an overflow list of C / 2
+  const int32_t Cb = (int32_t)std::min<int64_t>(
+      512, std::max<int64_t>(8, ((C + ix.ntiles - 1) / ix.ntiles + 7) / 8 * 8));
+  const int64_t Co = std::max<int64_t>(1, C / 2);
+  const int64_t per_q = (g.S + C + 2 * (int64_t)k + ix.ntiles * Cb + Co) * 8 + ix.ntiles * 4 +
+                        64 + 8 * (int64_t)k + (int64_t)radix_sort_scratch_bytes(k) + 64;
   int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));
   G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / C - 1));
   Scratch sc(st);
   uint64_t *skeys = nullptr, *theta = nullptr, *list = nullptr, *kth = nullptr, *keys = nullptr,
-           *alt = nullptr;
-  int32_t *cnt = nullptr, *fb = nullptr;
+           *alt = nullptr, *slots = nullptr, *ovf = nullptr;
+  int32_t *cnt = nullptr, *fb = nullptr, *slot_cnt = nullptr;
   char* tmp = nullptr;
+  LK_TRY(sc.get(&slots, G * ix.ntiles * Cb));
+  LK_TRY(sc.get(&slot_cnt, G * ix.ntiles));
+  LK_TRY(sc.get(&ovf, G * Co));
   LK_TRY(sc.get(&skeys, G * g.S));
   LK_TRY(sc.get(&theta, G));
   LK_TRY(sc.get(&list, G * C));
@@ -672,9 +823,12 @@ hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_querie
   LK_TRY(sc.get(&tmp, sort_bytes(G, k)));
   Workspace w = ws;  // the handle's claim counters, counters and segment table
   w.theta = theta;
-  w.list = list;
+  w.list = ovf;  // REST: the slots' overflow
   w.list_cnt = cnt;
-  w.list_cap = (int32_t)C;
+  w.list_cap = (int32_t)Co;
+  w.slots = slots;
+  w.slot_cnt = slot_cnt;
+  w.slot_cap = Cb;
   for (int64_t q0 = 0; q0 < Q; q0 += G) {
     const int64_t gq = std::min<int64_t>(G, Q - q0);
     const int32_t* q = d_queries + q0 * T;
@@ -682,15 +836,21 @@ hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_querie
     hipLaunchKernelGGL(row_kth_kernel<0>, dim3((unsigned)gq), dim3(kSelT), 0, st, skeys, g.S, cnt,
                        0, (uint32_t)k, ix.doc_offset, theta, fb + q0);
     LK_TRY(hipMemsetAsync(ws.counters, 0, sizeof(int32_t) * kCounters, st));
+    LK_TRY(hipMemsetAsync(slot_cnt, 0, sizeof(int32_t) * gq * ix.ntiles, st));
     LK_TRY(launch_rest_lists(ix, q, gq, T, g, w, st));
+    hipLaunchKernelGGL(slot_pack_kernel, dim3((unsigned)gq), dim3(kSelT), 0, st, slots, slot_cnt,
+                       ix.ntiles, Cb, ovf, (int32_t)Co, cnt, list, C);
     hipLaunchKernelGGL(row_kth_kernel<1>, dim3((unsigned)gq), dim3(kSelT), 0, st, list, C, cnt,
                        (int32_t)C, (uint32_t)k, 0ll, kth, fb + q0);
     hipLaunchKernelGGL(list_compact_kernel, dim3((unsigned)gq), dim3(kSelT), 0, st, list, C, cnt,
                        kth, fb + q0, (int64_t)k, keys);
-    const uint64_t* sorted = nullptr;
-    LK_TRY(sort_rows(keys, alt, gq, k, tmp, &sorted, st));
-    hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(gq * k, 256, 4096)), dim3(256), 0, st, sorted,
-                       (int64_t)k, gq, k, k, ix.doc_offset, d_docs + q0 * k, d_scores + q0 * k);
+    if (!lds_sort_write(keys, gq, k, k, ix.doc_offset, d_docs + q0 * k, d_scores + q0 * k, st)) {
+      const uint64_t* sorted = nullptr;
+      LK_TRY(sort_rows(keys, alt, gq, k, tmp, &sorted, st));
+      hipLaunchKernelGGL(lk_write_kernel, dim3(grid_for(gq * k, 256, 4096)), dim3(256), 0, st,
+                         sorted, (int64_t)k, gq, k, k, ix.doc_offset, d_docs + q0 * k,
+                         d_scores + q0 * k);
+    }
     LK_TRY(hipGetLastError());
   }
   // the queries the lists could not serve: the dense path, on their own (the

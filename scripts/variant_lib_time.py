@@ -26,7 +26,7 @@ if not os.path.exists(c + "_dt.npy"):
 ip, ix, dt = (np.load(c + "_" + n + ".npy", mmap_mode="r") for n in ("ip", "ix", "dt"))
 index = GpuIndex(np.ascontiguousarray(ip), ix, dt, hi - lo, doc_offset=lo)
 q = torch.from_numpy(synth.make_queries(cfg)).cuda()
-Q, k = q.shape[0], cfg.k
+Q, k = q.shape[0], int(os.environ.get("VK", cfg.k))
 d = torch.empty((Q, k), dtype=torch.int32, device="cuda"); s = torch.empty((Q, k), device="cuda")
 st = torch.cuda.current_stream()
 for _ in range(3):
@@ -40,7 +40,7 @@ torch.cuda.synchronize()
 h = int((d.to(torch.int64) * 1000003 + s.view(torch.int32).to(torch.int64)).sum().item())
 ss = index.search_stats()
 print(json.dumps({"lib": os.path.basename(_capi.LIB), "env": os.environ.get("VENV", ""),
-                  "cfg": os.environ.get("VCFG", "c3"), "terms": cfg.terms_per_query, "score_ms": round(p["score_ms"] / p["score_launches"], 4),
+                  "cfg": os.environ.get("VCFG", "c3"), "k": k, "terms": cfg.terms_per_query, "score_ms": round(p["score_ms"] / p["score_launches"], 4),
                   "total_ms": round(p["total_ms"] / p["searches"], 4), "hash": h,
                   "kernels": sorted(index.last_dispatch()["kernels"]),
                   "fallback_queries": ss["fallback_queries"],
