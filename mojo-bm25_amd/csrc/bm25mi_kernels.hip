@@ -732,6 +732,28 @@ __device__ __forceinline__ PostingRsrc posting_rsrc(const IndexArgs& a) {
   r.val = __builtin_amdgcn_make_buffer_rsrc((void*)a.val, 0, (int)((uint32_t)np * 4u), 0x00020000);
   return r;
 }
+// The flat kernel's row loads as STRUCTURED buffer loads: records of one
+// lane's pair (4 B of ldoc, 8 B of val), the record index in a VGPR, the
+// row's first pair as soffset (outside the range check).  One clamped index
+// then serves both loads: lanes past the row's last valid one reload that
+// lane's pair, so a short segment's row touches no cache line of its
+// neighbours (the struct form has no builtin: the intrinsic by name).
+typedef uint32_t bm25_v2u __attribute__((ext_vector_type(2)));
+__device__ uint32_t bm25_sload_b32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
+                                   int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i32");
+__device__ bm25_v2u bm25_sload_b64(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
+                                   int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v2i32");
+
+__device__ __forceinline__ PostingRsrc posting_rsrc_pairs(const IndexArgs& a) {
+  PostingRsrc r;
+  // num_records = whole pairs (a row's clamped index stays below its row's
+  // last posting, so below this); stride 4 B (two u16 slots) / 8 B (two f32)
+  const int np2 = (int)((a.nnz + kPostingPad) >> 1);
+  r.ldoc = __builtin_amdgcn_make_buffer_rsrc((void*)a.ldoc, 4, np2, 0x00020000);
+  r.val = __builtin_amdgcn_make_buffer_rsrc((void*)a.val, 8, np2, 0x00020000);
+  return r;
+}
+
 // Dense form (heavier items): every accumulator of the tile (docs past n_docs
 // excluded), then the accumulators are cleared.  Lane entries are in doc
 // order inside each lane (entry_doc), so a slice is a contiguous run of them.
@@ -935,8 +957,8 @@ constexpr int kQW = 4;
 #define BM25_FLAT_WPE 5
 #endif
 
-#ifndef BM25_CLAMP  // row loads of idle lanes kept inside the row's valid lanes
-#define BM25_CLAMP 0
+#ifndef BM25_CLAMP  // row loads of idle lanes kept inside the row's valid lanes: 2 by
+#define BM25_CLAMP 2  // a record index (one VALU min), 1 by byte offsets, 0 not at all
 #endif
 
 #ifndef BM25_TRACE  // dev variant builds: per-wave start / end clocks of the REST pass
@@ -1034,7 +1056,10 @@ __device__ __forceinline__ FlatTab flat_chunk(uint32_t sb, uint32_t sl, uint32_t
   const uint32_t tile = (uint32_t)pos >> TL;
   uint32_t tp = (uint32_t)__shfl_up((int)tile, 1, 64);
   if (lane == 0u) tp = prev;
-  t.w = masks | ((in && tile != tp) ? kRowNewTile : 0u) | (tile << 18) | (par ? kRowParity : 0u);
+  // bits 26-31: the row's last lane with a valid slot (top - 1; 0 for empty rows)
+  const uint32_t top1 = masks != 0u ? (((rhi + 1u) >> 1) - 1u) : 0u;
+  t.w = masks | ((in && tile != tp) ? kRowNewTile : 0u) | (tile << 18) | (par ? kRowParity : 0u) |
+        (top1 << 26);
   t.last = lane_u32(tile, 63);
   return t;
 }
@@ -1091,7 +1116,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       ctr[kDoneOff] = 0;
     }
   };
+#if BM25_CLAMP == 2
+  const PostingRsrc pr = posting_rsrc_pairs(a);
+#else
   const PostingRsrc pr = posting_rsrc(a);
+#endif
 #if BM25_TRACE
   const uint64_t tr_t0 = wall_clock64();
   uint32_t tr_items = 0, tr_rows = 0;
@@ -1329,6 +1358,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     if (il == nI) next_chunk();
     const uint32_t base = lane_u32(tI.base, (int)il);
     wR[s] = lane_u32(tI.w, (int)il);
+#if BM25_CLAMP == 2
+    const int li2 = (int)min(lane, wR[s] >> 26);  // (row word bits 26-31: top - 1)
+    ldR[s] = bm25_sload_b32(pr.ldoc, li2, 0, (int)base, 0);
+    const bm25_v2u v = bm25_sload_b64(pr.val, li2, 0, (int)(base * 2u), 0);
+    v0R[s] = __uint_as_float(v[0]);
+    v1R[s] = __uint_as_float(v[1]);
+#else
 #if BM25_CLAMP
     // lanes past the row's last valid one load that lane's pair again: the
     // row touches no cache line beyond its segment's (a short segment's row
@@ -1344,6 +1380,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr.val, (int)lo8, (int)(base * 2u), 0);
     v0R[s] = __uint_as_float((uint32_t)v[0]);
     v1R[s] = __uint_as_float((uint32_t)v[1]);
+#endif
     ++il;
   };
 #pragma unroll

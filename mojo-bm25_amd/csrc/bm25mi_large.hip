@@ -707,6 +707,7 @@ __global__ __launch_bounds__(kSelT) void slot_pack_kernel(const uint64_t* __rest
                                                           uint64_t* __restrict__ list, int64_t C) {
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t s_tot;
+  __shared__ uint32_t offs[kSelT];
   const int64_t row = blockIdx.x;
   const int32_t* cn = slot_cnt + row * ntiles;
   const uint64_t* sl = slots + row * ntiles * Cb;
@@ -721,12 +722,22 @@ __global__ __launch_bounds__(kSelT) void slot_pack_kernel(const uint64_t* __rest
     const int64_t t = t0 + threadIdx.x;
     const uint32_t n = t < ntiles ? (uint32_t)min(cn[t], Cb) : 0u;
     const uint32_t ex = block_excl256(n, wsum);
-    const uint32_t at = carry + ex;
-    for (uint32_t i = 0; i < n; ++i)
-      if ((int64_t)(at + i) < C) out[at + i] = sl[t * Cb + i];
+    offs[threadIdx.x] = ex;
     if (threadIdx.x == kSelT - 1) s_tot = ex + n;
     __syncthreads();
-    carry += s_tot;
+    // the round's keys copied by all threads at once (independent loads): key
+    // e is in the last slot whose offset is <= e
+    const uint32_t tot = s_tot;
+    for (uint32_t e = threadIdx.x; e < tot; e += kSelT) {
+      uint32_t lo = 0u, hi = kSelT - 1u;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1u) >> 1;
+        if (offs[mid] <= e) lo = mid;
+        else hi = mid - 1u;
+      }
+      if ((int64_t)(carry + e) < C) out[carry + e] = sl[(t0 + lo) * Cb + (e - offs[lo])];
+    }
+    carry += tot;
     __syncthreads();
   }
   for (int32_t i = threadIdx.x; i < no; i += kSelT)
