@@ -45,6 +45,10 @@ for W in (1, 8):
                           "rows_mean_max": [float(b[:, 3].mean()), int(b[:, 3].max())],
                           "late_waves_rows_mean": float(b[late, 3].mean()),
                           "late_waves_items_mean": float(b[late, 2].mean()),
-                          "busy_fraction": round(float((en - st).sum() / (span * used.sum())), 3)}),
+                          "busy_fraction": round(float((en - st).sum() / (span * used.sum())), 3),
+                          # per XCD (workgroup i runs on XCD i % 8): end p50 / max, rows
+                          "xcd_end_p50_max_rows": [[round(pct(en[xs], 50), 1), round(float(en[xs].max()), 1),
+                                                    int(b[xs, 3].sum())]
+                                                   for xs in (np.nonzero(used)[0] % 8 == x for x in range(8))]}),
               flush=True)
     index.close()
