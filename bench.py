@@ -313,6 +313,17 @@ def main():
     prof = index.profile_read()
     dispatch = index.last_dispatch()
     stats = index.search_stats()  # the last timed search's selection counters
+    if info.get("tile_bounds"):
+        # the (query, tile) pairs the tile bound skipped and their postings:
+        # counted by the count_skips REST build (registers the timed build does
+        # without), in one extra search of the same batch after the timed ones
+        index.set_option("count_skips", 1)
+        step()
+        torch.cuda.synchronize(dev)
+        counted = index.search_stats()
+        stats["bound_skipped_tiles"] = counted["bound_skipped_tiles"]
+        stats["bound_skipped_postings"] = counted["bound_skipped_postings"]
+        index.set_option("count_skips", 0)
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     # end-to-end (N=1): the host-buffer entry point bm25_search — H2D of the
     # query batch, the search, D2H of the [Q, k] results — timed per call
@@ -363,7 +374,7 @@ def main():
     # tile-bound skip spared (the kernel never reads those postings, so the
     # algorithmic rate is partly an effective rate), the batch's distinct
     # posting bytes (the reuse floor) and the counter-measured bytes
-    skip_post = int(stats.get("bound_skipped_postings", 0))
+    skip_post = max(0, int(stats.get("bound_skipped_postings", 0)))
     n_post = query_postings(indptr, queries)
     distinct = batch_distinct_postings(indptr, queries)
     read_bytes = alg_bytes - 8 * skip_post
@@ -421,8 +432,12 @@ def main():
                 "traffic_source": (f"profiles/traffic.json ({traffic.get('source')}): "
                                    f"{traffic.get('method')}; L2 hit rate "
                                    f"{traffic.get('l2_hit_rate')}") if traffic else None,
-                "kernel": ("large-k search (scores_batch_kernel dense sums + lk_* radix "
-                           "selection + hipCUB segmented sort)" if large_k else
+                "kernel": (("large-k list path (score_flat_kernel SAMPLE slice maxima + "
+                            "row_kth_kernel theta + score_flat_kernel REST crossing lists into "
+                            "per-tile slots + slot_pack / row_kth / list_compact + LDS row sort)")
+                           if large_k and "flat_rest" in dispatch["kernels"] else
+                           "large-k search (scores_batch_kernel dense sums + lk_* radix "
+                           "selection + row sort)" if large_k else
                            "score pass (bound_keys_kernel tile-bound threshold + "
                            "score_flat_kernel REST)" if "bound_keys" in dispatch["kernels"] else
                            "score pass (score_flat_kernel SAMPLE + theta_wave_kernel + "
@@ -433,15 +448,16 @@ def main():
                                   "time, including postings the REST tile skip never reads"
                                   if skip_post > 0 else
                                   "algorithmic bytes (SURVEY.md §8(d)) over the pass time"),
-                "bound_skip": {"pairs": int(stats.get("bound_skipped_tiles", 0)),
+                "bound_skip": {"pairs": max(0, int(stats.get("bound_skipped_tiles", 0))),
                                "postings": skip_post,
                                "share_of_postings": round(skip_post / max(n_post, 1), 4),
                                "read_bytes": read_bytes,
                                "read_frac": round(read_bytes / (kern_ms * 1e-3) / 1e9
                                                   / HBM_PEAK_GBPS, 4),
                                "note": "postings of the (query, tile) pairs whose term-maxima "
-                                       "sum stayed below theta (last timed search); read_bytes "
-                                       "= algorithmic minus 8 B per skipped posting"},
+                                       "sum stayed below theta (counted in one more search "
+                                       "of the batch by the count_skips build); read_bytes = "
+                                       "algorithmic minus 8 B per skipped posting"},
                 "batch_distinct_bytes": {"postings": distinct, "at_6B": 6 * distinct,
                                          "at_8B": 8 * distinct,
                                          "reuse": round(n_post / max(distinct, 1), 2),

@@ -319,7 +319,8 @@ int bm25_search_stats(bm25_index* idx, int64_t* rescored_tiles,
                       int64_t* fallback_queries);
 /* The same plus *bound_skipped: (query, tile) pairs the REST pass skipped
  * because the sum of the query terms' largest scores in the tile (the tile
- * bounds of a dense, non-negative index) is below the query's threshold.
+ * bounds of a dense, non-negative index) is below the query's threshold —
+ * counted only by a search with the count_skips option on, else -1.
  * Any pointer may be NULL. */
 int bm25_search_stats_ex(bm25_index* idx, int64_t* rescored_tiles,
                          int64_t* fallback_queries, int64_t* bound_skipped);
@@ -327,7 +328,9 @@ int bm25_search_stats_ex(bm25_index* idx, int64_t* rescored_tiles,
  *   [0] tiles re-scored exactly, [1] queries sent to the exact fallback
  *   stage, [2] (query, tile) pairs the REST pass skipped by their tile
  *   bound, [3] the postings of those skipped (query, tile) segments (what
- *   the skip saved of the algorithmic bytes, 8 B each), [4] queries left to
+ *   the skip saved of the algorithmic bytes, 8 B each) — [2] and [3]
+ *   counted only by a search with the count_skips option on, else -1 —
+ *   [4] queries left to
  *   the block merge (lists longer than one wavefront's registers), [5] k >
  *   4096: queries the list path handed to dense score rows (-1: the dense
  *   path served the whole search).
@@ -338,7 +341,7 @@ int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
  * Search options of one handle.  A new handle takes them from the
  * environment (BM25_FLAT, BM25_FLAT_BW, BM25_ITEMS_PER_WAVE, BM25_SAMPLE_P,
  * BM25_LIST_CAP, BM25_CLAIM_CH, BM25_CLAIM_M, BM25_TILE_BOUND, BM25_THETA_BOUND,
- * BM25_GRID_PCT, BM25_LARGE_LISTS) at
+ * BM25_GRID_PCT, BM25_LARGE_LISTS, BM25_COUNT_SKIPS) at
  * bm25_index_create; these
  * calls change or read them afterwards, effective from the next search.
  * Results never depend on them (every setting is bit-exact); they choose
@@ -367,6 +370,11 @@ int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
  *                    applies (a sampled threshold, keys above it listed by the
  *                    REST pass, selected and sorted — no dense score rows);
  *                    0: dense score rows for every query
+ *   "count_skips"    1: the REST pass also counts the (query, tile) pairs its
+ *                    tile bound skips and their postings (bm25_search_counters
+ *                    [2], [3]) — a kernel build of its own: the two counts'
+ *                    registers cost the pass 13 % on an 8-way doc shard;
+ *                    0 (default): not counted
  *   "grid_pct"       percent of the device's resident workgroup slots the
  *                    persistent score kernels launch (1..100, default 100):
  *                    below 100 leaves slots for kernels of another stream

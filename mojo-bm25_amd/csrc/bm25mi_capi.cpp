@@ -141,6 +141,7 @@ SearchOpts env_opts() {
   o.tile_bound = env_int("BM25_TILE_BOUND", o.tile_bound) != 0;
   o.theta_bound = env_int("BM25_THETA_BOUND", o.theta_bound) != 0;
   o.grid_pct = std::min(100, std::max(1, env_int("BM25_GRID_PCT", o.grid_pct)));
+  o.count_skips = env_int("BM25_COUNT_SKIPS", o.count_skips) != 0;
   o.large_lists = env_int("BM25_LARGE_LISTS", o.large_lists) != 0;
   return o;
 }
@@ -180,6 +181,9 @@ int set_opt(SearchOpts& o, const char* name, int64_t v) {
   } else if (n == "large_lists") {
     if (v != 0 && v != 1) return fail(BM25_EINVAL, "large_lists must be 0 or 1");
     o.large_lists = (int)v;
+  } else if (n == "count_skips") {
+    if (v != 0 && v != 1) return fail(BM25_EINVAL, "count_skips must be 0 or 1");
+    o.count_skips = (int)v;
   } else if (n == "grid_pct") {
     if (v < 1 || v > 100) return fail(BM25_EINVAL, "grid_pct must be in 1..100");
     o.grid_pct = (int)v;
@@ -202,6 +206,7 @@ int get_opt(const SearchOpts& o, const char* name, int64_t* v) {
   else if (n == "tile_bound") *v = o.tile_bound;
   else if (n == "theta_bound") *v = o.theta_bound;
   else if (n == "grid_pct") *v = o.grid_pct;
+  else if (n == "count_skips") *v = o.count_skips;
   else if (n == "large_lists") *v = o.large_lists;
   else return fail(BM25_EINVAL, "unknown option '%s'", name);
   return BM25_OK;
@@ -1112,7 +1117,7 @@ int bm25_search_stats_ex(bm25_index* h, int64_t* rescored_tiles, int64_t* fallba
   read_counters(h, cnt);
   if (rescored_tiles) *rescored_tiles = cnt[3];
   if (fallback_queries) *fallback_queries = cnt[2];
-  if (bound_skipped) *bound_skipped = cnt[5];
+  if (bound_skipped) *bound_skipped = (h->ix.disp.kernels & kKCountSkips) ? cnt[5] : -1;
   return BM25_OK;
 }
 
@@ -1125,7 +1130,10 @@ int bm25_search_counters(bm25_index* h, int64_t* out, int32_t n) {
   read_counters(h, cnt);
   uint64_t post = 0;
   std::memcpy(&post, cnt + 6, sizeof post);  // counters[6..7]: a u64 (score_flat_kernel)
-  const int64_t v[6] = {cnt[3], cnt[2], cnt[5], (int64_t)post, cnt[4], h->large_fallback};
+  // (the skipped pairs and postings: counted by the count_skips build only, else -1)
+  const bool counted = (h->ix.disp.kernels & kKCountSkips) != 0;
+  const int64_t v[6] = {cnt[3], cnt[2], counted ? cnt[5] : -1, counted ? (int64_t)post : -1,
+                        cnt[4], h->large_fallback};
   for (int i = 0; i < n; ++i) out[i] = v[i];
   return BM25_OK;
 }

@@ -77,6 +77,7 @@ struct SearchOpts {
   int tile_bound = 1;      // REST skips tiles whose term-maxima sum is below theta (needs bmax)
   int theta_bound = 1;     // threshold keys from the tile bounds instead of a SAMPLE pass
                            // (needs bmax; search_geom)
+  int count_skips = 0;     // REST counts the postings its tile bound skips (a build of its own)
   int grid_pct = 100;      // percent of the resident slots the persistent score kernels take
   int large_lists = 1;     // k > kMaxK: the list path (0: dense score rows for every query)
 };
@@ -89,6 +90,7 @@ enum {
   kKBound = 128, // tile-bound threshold keys (bound_keys_kernel) instead of a SAMPLE pass
   kKBoundOff = 256,  // (not a kernel) the tile-bound threshold was off for this search:
                      // earlier ones overflowed with it (DevIndex::bound_weak)
+  kKCountSkips = 512,  // (a flag) REST counted the postings its tile bound skipped
 };
 struct Dispatch {
   uint32_t kernels = 0;       // kK* bits of the score kernels launched

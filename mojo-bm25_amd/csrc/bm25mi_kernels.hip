@@ -162,6 +162,30 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
          (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+// Sum over each group of 2^TL consecutive lanes (a flat-kernel tile's term
+// lanes), every lane of the group getting it: DPP inside 16-lane rows (no LDS
+// round trip, unlike __shfl_xor's ds_bpermute), shuffles above.
+template <int TL>
+__device__ __forceinline__ uint32_t seg_sum_u32(uint32_t v) {
+  if (TL >= 1) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+  if (TL >= 2) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+  if (TL >= 3) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if (TL >= 4) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  if (TL >= 5) v += (uint32_t)__shfl_xor((int)v, 16, 64);
+  if (TL >= 6) v += (uint32_t)__shfl_xor((int)v, 32, 64);
+  return v;
+}
+template <int TL>
+__device__ __forceinline__ float seg_sum_f32(float v) {
+  if (TL >= 1) v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  if (TL >= 2) v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  if (TL >= 3) v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  if (TL >= 4) v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));
+  if (TL >= 5) v += __shfl_xor(v, 16, 64);
+  if (TL >= 6) v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
 // Bitwise OR over the 64 lanes (DPP inside rows, then SGPRs); AND as ~OR(~x).
 __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
   v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
@@ -1215,7 +1239,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   };
 
   uint32_t nbound = 0;  // REST: (query, tile) pairs this lane's tiles skipped by their bound
-  uint32_t npost = 0;   // ... and the postings of this lane's skipped segments
+  // ... and the postings of this lane's skipped segments.  Both only in the
+  // REST build of the count_skips option (SM == 2): the two live registers
+  // cost the pass 13 % on an 8-way doc shard (profiles/r05/counters)
+  constexpr bool kCountPost = PH == kRest && SM == 2;
+  uint32_t npost = 0;
   // ---- the issue side's item: its segments (lane s = tile * TT + term) and
   // row numbering; the item prefetch pipeline one and two items ahead
   uint32_t iSb = 0, iSl = 0, iIncl = 0, iExcl = 0;
@@ -1242,16 +1270,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       // of these maxima; the 1e-4 margin covers this tree-order sum's own
       // rounding.  The tile runs no rows and no epilogue.
       if (a.bmax != nullptr && th_pos) {
-        float ub = f16_bits_to_float((uint16_t)dN.aux);
-#pragma unroll
-        for (int o = 1; o < (int)TT; o <<= 1) ub += __shfl_xor(ub, o, 64);
+        const float ub = seg_sum_f32<TL>(f16_bits_to_float((uint16_t)dN.aux));
         const bool cut = ub * 1.0001f < key_score((uint32_t)(thN >> 32));
         // ... the tile's postings (lanes outside the item hold r1 == r0), counted
-        // with the pair by the tile's first term lane
-        uint32_t tp = dN.r1 - dN.r0;
-#pragma unroll
-        for (int o = 1; o < (int)TT; o <<= 1) tp += (uint32_t)__shfl_xor((int)tp, o, 64);
-        if (cut && !skip && lt == 0u && (int)li < nx.bw) {
+        // with the pair by the tile's first term lane (the count_skips build)
+        const uint32_t tp = kCountPost ? seg_sum_u32<TL>(dN.r1 - dN.r0) : 0u;
+        if (kCountPost && cut && !skip && lt == 0u && (int)li < nx.bw) {
           ++nbound;
           npost += tp;
         }
@@ -1268,9 +1292,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     if constexpr (PH == kSample) {
       // a sample tile of the item without any posting row runs no epilogue:
       // its keys are written here (0: no positive sum)
-      uint32_t tr = nr;
-#pragma unroll
-      for (int o = 1; o < (int)TT; o <<= 1) tr += (uint32_t)__shfl_xor((int)tr, o, 64);
+      const uint32_t tr = seg_sum_u32<TL>(nr);
       if (lt == 0u && (int)li < nx.bw && tr == 0u) {
         uint64_t* out = cand + (int64_t)nx.q * cstride + (int64_t)(nx.b * BW + (int32_t)li) * SM;
 #pragma unroll
@@ -1534,7 +1556,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   }
 #endif
   if (curTi != kNoTile) epilogue();
-  if (PH == kRest && stats != nullptr) {  // bound-skipped tiles (and postings) of this wave
+  if (kCountPost && stats != nullptr) {  // bound-skipped tiles and postings of this wave
     const uint32_t nb = wave_sum_u32(nbound);
     if (lane == 0 && nb != 0u) atomicAdd(stats, (int32_t)nb);
     // stats + 1 .. + 2: a u64 count (Workspace::counters[6..7], 8-B aligned)
@@ -3093,6 +3115,7 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
     const int claim_m = std::max(1, std::min(ix.opt.claim_m, grid / 8));
     const int bw = flat_band(ix.opt, nt, sg.nq_host, grid, 64 >> TL, sg.nq_dev != nullptr);
     ix.disp.kernels |= PH == kSample ? kKFlatSample : (PH == kRest ? kKFlatRest : kKFlatAll);
+    if (PH == kRest && SM == 2) ix.disp.kernels |= kKCountSkips;
     ix.disp.term_lanes = 1 << TL;
     ix.disp.band_tiles[PH] = bw;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, st, a, q, (int32_t)T, sg.P,
@@ -3131,9 +3154,12 @@ static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t T, int64_
       if (sg.M == kTileM) return launch_flat_tl<S, PH, kTileM>(ix, q, T, Qb, sg, ws, st);
       if (sg.M == kLargeM) return launch_flat_tl<S, PH, kLargeM>(ix, q, T, Qb, sg, ws, st);
     }
-    if constexpr (PH == kRest)  // the large-k list path's slots
-      if (sg.M == kLargeM && ws.slots != nullptr)
+    if constexpr (PH == kRest) {
+      if (sg.M == kLargeM && ws.slots != nullptr)  // the large-k list path's slots
         return launch_flat_tl<S, PH, kLargeM>(ix, q, T, Qb, sg, ws, st);
+      if (ix.opt.count_skips)  // the build that counts the skipped postings
+        return launch_flat_tl<S, PH, 2>(ix, q, T, Qb, sg, ws, st);
+    }
     return launch_flat_tl<S, PH, 1>(ix, q, T, Qb, sg, ws, st);
   }
   int32_t* wctr = ws.wctr + (int64_t)sg.ctr_region * kWctrInts;

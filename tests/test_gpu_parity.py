@@ -511,7 +511,7 @@ def test_options_rejected(gpu):
     ip = np.array([0, 1], np.int32)
     index = _idx(ip, np.array([0], np.int32), np.array([1.0], np.float32), 1)
     for name, val in (("flat", 2), ("flat_bw", 3), ("sample_p", 3), ("claim_m", 9),
-                      ("nope", 1)):
+                      ("count_skips", 2), ("nope", 1)):
         with pytest.raises(ValueError):
             index.set_option(name, val)
 
@@ -1200,10 +1200,16 @@ def test_tile_bound_skips_exact(gpu, T):
     q[1, 1:] = q[1, 0]
     index = _idx(ip, ix, dt, N, segments="dense")
     assert index.get_option("tile_bound") == 1
+    _exact(index.search(q, 10), oracle.search_c(N, ip, ix, dt, q, 10, threads=8))
+    # the skipped postings are counted by the count_skips build only
+    assert index.search_stats()["bound_skipped_postings"] == -1
+    assert "count_skips" not in index.last_dispatch()["kernels"]
+    index.set_option("count_skips", 1)
     for k in (10, 100):
         ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
         _exact(index.search(q, k), ref)
         st = index.search_stats()
+        assert "count_skips" in index.last_dispatch()["kernels"]
         skipped = st["bound_skipped_tiles"]
         assert skipped > 0, skipped
         # the postings of the skipped pairs (bench.py's roofline.bound_skip): the
