@@ -28,7 +28,9 @@ constants are stated in the output line.  Two ways to add them:
   python scripts/shard_probe.py [W ...]     (env VLIB: a variant library;
       PROBE_Q: batch size; PROBE_RANKS, PROBE_ITERS; PROBE_PARTS: e.g. "1,2,4";
       PROBE_GRID: grid_pct values, e.g. "100,90"; PROBE_HYBRID=1: also the
-      2-replica x W/2-shard split, each rank Q/2 queries on a 2/W shard)
+      2-replica x W/2-shard split, each rank Q/2 queries on a 2/W shard;
+      PROBE_PIPE=2: two batches in flight per rank, on the handle and a fork
+      with their own streams, collectives inline on one comm stream)
 """
 import json
 import os
@@ -119,6 +121,36 @@ def rank_parts(shards, r, q, k, W, smax, keys_p, g_p, rows, out_d, out_s, forks,
         main.wait_event(e)
 
 
+def rank_pipelined(shards, forks, r, q, k, W, smax, keys_c, g_c, outs, streams, comm, keys_us,
+                   list_us, step):
+    """One rank's batch number `step` with PROBE_PIPE batches in flight: the
+    batch runs on context step % PIPE (the shard's handle or one of its forks,
+    each with its own stream, keys, lists and outputs), so the next batch's
+    kernels start while this one's tail, merges and collectives finish.  The
+    modelled collectives are spin kernels on the one communication stream,
+    ordered by events as bm25mi.dist orders the real ones."""
+    i = step % len(streams)
+    ctx = ([shards[r]] + forks)[i]
+    st, kk, g = streams[i], keys_c[i], g_c[i]
+    dev = q.device.index
+
+    def coll(us):
+        e = torch.cuda.Event()
+        e.record(st)
+        comm.wait_event(e)
+        sleep_us(us, comm)
+        e2 = torch.cuda.Event()
+        e2.record(comm)
+        st.wait_event(e2)
+
+    ctx.search_sample_device(q, k, W, smax, kk[r], st)
+    coll(keys_us)
+    ctx.search_finish_device(q, k, W, smax, kk, g[r, 0], g[r, 1].view(torch.float32), st)
+    coll(list_us)
+    merge_sorted_device(dev, g, g[:, 1].view(torch.float32), W, q.shape[0], k,
+                        2 * q.shape[0] * k, outs[i][0], outs[i][1], st)
+
+
 def main():
     cfg = synth.CONFIGS["c3"]
     nq = int(os.environ.get("PROBE_Q", "0")) or None  # batch size (default: the config's 1024)
@@ -130,6 +162,7 @@ def main():
     parts_list = [int(x) for x in os.environ.get("PROBE_PARTS", "1").split(",")]
     grids = [int(x) for x in os.environ.get("PROBE_GRID", "100").split(",")]
     hybrid = os.environ.get("PROBE_HYBRID") == "1"
+    pipe = int(os.environ.get("PROBE_PIPE", "1"))  # batches in flight per rank
     w1_ms = None
     jobs = [(int(x), 1) for x in (sys.argv[1:] or ["1", "2", "4", "8"])]
     if hybrid:  # 2 replicas x W/2 shards: each rank half the batch on a 2/W shard
@@ -157,7 +190,18 @@ def main():
                 cuts = [Q * i // P for i in range(P + 1)]
                 rows = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
                 inline = P > 1 or os.environ.get("PROBE_INLINE") == "1"
-                if W == 1 and P == 1:
+                if W == 1 and P == 1 and pipe > 1:  # batches in flight on forks, own streams
+                    wforks = [shards[0]] + [shards[0].fork() for _ in range(pipe - 1)]
+                    wstreams = [torch.cuda.Stream() for _ in range(pipe)]
+                    wouts = [(torch.empty_like(out_d), torch.empty_like(out_s))
+                             for _ in range(pipe)]
+                    wstep = [0]
+
+                    def one(r):
+                        i = wstep[0] % pipe
+                        wforks[i].search_device(q, k, wouts[i][0], wouts[i][1], wstreams[i])
+                        wstep[0] += 1
+                elif W == 1 and P == 1:
                     def one(r):
                         shards[0].search_device(q, k, out_d, out_s, st)
                 else:
@@ -175,7 +219,25 @@ def main():
                         keys_p.append(kk)
                         g_p.append(g)
                     torch.cuda.synchronize()
-                    if inline:
+                    if pipe > 1:
+                        pforks = {}
+                        pstreams = [torch.cuda.Stream() for _ in range(pipe)]
+                        pcomm = torch.cuda.Stream()
+                        kus = model_gather_us(keys_b, W)
+                        lus = model_gather_us(list_b, W)
+                        keys_c = [keys_p[0]] + [keys_p[0].clone() for _ in range(pipe - 1)]
+                        g_c = [g_p[0]] + [g_p[0].clone() for _ in range(pipe - 1)]
+                        outs = [(torch.empty_like(out_d), torch.empty_like(out_s))
+                                for _ in range(pipe)]
+                        pstep = [0]
+
+                        def one(r):
+                            if r not in pforks:
+                                pforks[r] = [shards[r].fork() for _ in range(pipe - 1)]
+                            rank_pipelined(shards, pforks[r], r, q, k, W, smax, keys_c, g_c, outs,
+                                           pstreams, pcomm, kus, lus, pstep[0])
+                            pstep[0] += 1
+                    elif inline:
                         forks = {}
                         streams = [torch.cuda.Stream() for _ in rows]
                         comm = torch.cuda.Stream()
@@ -211,11 +273,13 @@ def main():
                     per_rank.append({"rank": r, "ms": round(ms, 4),
                                      "fallback_queries": shards[r].search_stats()["fallback_queries"]})
                 worst = max(x["ms"] for x in per_rank)
+                inline = inline or pipe > 1
                 coll_us = 0.0 if inline else (model_gather_us(keys_b, W) + model_gather_us(list_b, W))
                 proj = worst + coll_us * 1e-3
                 if W == 1 and P == 1 and R == 1 and gp == 100:
                     w1_ms = worst
                 line = {"W": W * R, "shards": W, "replicas": R, "parts": P, "grid_pct": gp,
+                        "batches_in_flight": pipe if W > 1 else 1,
                         "queries_per_rank": Q, "shard_docs_max": smax, "sample_width": S,
                         "per_rank": per_rank, "max_rank_ms": round(worst, 4),
                         "model": {"alpha_us": ALPHA_US, "link_GBps": LINK_GBS,
