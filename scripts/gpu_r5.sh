@@ -5,6 +5,7 @@
 #   STEPS=lines   bench lines: c3 (CPU legs), c2 (CPU legs), replica proxy
 #                 (rank 0 of 8), c3 at k=10000 (large-k path), c3 at 16
 #                 terms, c5 (one rank's shard)
+#   STEPS=prof    rocprofv3 kernel traces (c3, k=10000) and PMC traffic passes
 #   STEPS=probe   scripts/shard_probe.py (W = PROBE_WS)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -49,6 +50,27 @@ for step in ${STEPS:-tests lines}; do
       VCFG=${cfg%%:*} VTERMS=$([ "${cfg#*:}" != "$cfg" ] && echo ${cfg#*:}) timeout -k 10 900 python -u scripts/variant_lib_time.py $VLIBS > $OUT/variants_${cfg/:/_t}.jsonl 2> $OUT/variants_${cfg/:/_t}.err || { echo variants failed; tail -20 $OUT/variants_${cfg/:/_t}.err; exit 1; }
       cat $OUT/variants_${cfg/:/_t}.jsonl
     done
+    ;;
+  prof)  # rocprofv3 kernel trace + stats of the c3 and k=10000 bench commands; PMC
+         # passes (one counter group per run) of the score kernels: c3, 16 terms, c5 shard
+    ( export TMPDIR=/tmp; cd /tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_c3 -o run -- python3 $R/bench.py --cpu-queries 0 --e2e-batches 0 > $OUT/bench_c3_rocprof.json 2> $OUT/bench_c3_rocprof.err || { echo trace c3 failed; exit 1; }
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_k10000 -o run -- python3 $R/bench.py --k 10000 --steps 5 --warmup 2 --cpu-queries 0 --e2e-batches 0 > $OUT/bench_k10000_rocprof.json 2> $OUT/bench_k10000_rocprof.err || { echo trace k10000 failed; exit 1; }
+      while read -r tag args ctrs; do
+        [ -z "$ctrs" ] && continue
+        timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-include-regex "score_flat|bound_keys" --output-format csv -d $OUT/pmc_${tag}_${ctrs%% *} -o pmc -- python3 $R/scripts/pmc_workload.py ${args//,/ } > $OUT/pmc_${tag}_${ctrs%% *}.log 2>&1 || { echo pmc $tag failed; exit 1; }
+      done <<'CTRS'
+c3 --config,c3 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum
+c3 --config,c3 WRITE_SIZE
+c3 --config,c3 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU
+c3 --config,c3 SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE
+t16 --config,c3,--terms,16 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum
+t16 --config,c3,--terms,16 WRITE_SIZE
+c5 --config,c5 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum
+c5 --config,c5 WRITE_SIZE
+CTRS
+    ) || exit 1
+    echo prof done
     ;;
   probe)  # per-rank config-3 shard work with real sample keys + modelled collectives
     timeout -k 10 900 python -u scripts/shard_probe.py ${PROBE_WS:-1 2 4 8} > $OUT/shard_probe.jsonl 2> $OUT/shard_probe.err || { echo probe failed; tail -20 $OUT/shard_probe.err; exit 1; }
