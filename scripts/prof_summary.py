@@ -19,7 +19,7 @@ d = args[0] if args else "gpurun_out"
 traffic_out = sys.argv[sys.argv.index("--traffic") + 1] if "--traffic" in sys.argv else None
 if traffic_out in args:
     args.remove(traffic_out)
-for f in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):
+for f in sorted(glob.glob(os.path.join(d, "trace*", "*kernel_stats.csv"))):
     print("== kernel stats", os.path.relpath(f, d))
     for r in csv.DictReader(open(f)):
         name = r["Name"].split("(")[0].replace("void ", "").replace("bm25mi::", "")
@@ -72,7 +72,7 @@ if traffic_out:
                         "l2_hit_rate": round(hit / max(hit + miss, 1), 3),
                         "phases": sorted(ph)})
     json.dump({"source": os.path.relpath(d), "kernels": "the score pass of one search: bound_keys_kernel or score_flat_kernel SAMPLE, score_flat_kernel REST (+ the fallback ALL launch)",
-               "method": ("rocprofv3 --pmc, one counter group per pass (scripts/gpu_evidence.sh PART=prof); "
+               "method": ("rocprofv3 --pmc, one counter group per pass (scripts/gpu_r5.sh STEPS=prof); "
                           "read bytes = TCC_EA0_RDREQ x 128 B, the bytes per request measured for this "
                           "kernel's 4-B and 8-B-per-lane buffer loads by the calibration kernel "
                           "(profiles/r02/traffic_calib/summary.json: 128.0 B/RDREQ, FETCH_SIZE reports "
