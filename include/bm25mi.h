@@ -124,7 +124,10 @@ int bm25_index_bounds(const bm25_index* idx, int32_t* has_bounds, int64_t* bytes
  *   out_scores [Q, k] f32
  * Every 0 <= k <= n_docs is served (k > 4096 by the exact large-k path: a
  * sampled threshold, the keys above it listed, selected and sorted — or
- * dense score rows with a radix selection where lists cannot serve).
+ * dense score rows with a radix selection where lists cannot serve).  That
+ * path's scratch (up to a quarter of the free device memory, at most 4 GiB)
+ * stays with the handle after its first such search, for the next ones,
+ * until bm25_index_destroy.
  * Errors: EINVAL when a token id >= n_terms (message matches
  * bm25_native.py:118-121), when k < 0 or k > n_docs.
  */

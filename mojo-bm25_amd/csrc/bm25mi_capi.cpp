@@ -99,6 +99,7 @@ struct bm25_index {
   int64_t last_bound_q = 0;
   int64_t large_fallback = 0;  // queries of the last large-k list search taken by dense rows
                                // (-1: the dense path served the whole search)
+  LargeArena arena;            // the large-k paths' scratch (grown to what they last asked for)
 };
 
 namespace {
@@ -385,6 +386,18 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
       const int rc = ensure_ws(h, Q, T, 1);  // claim counters, counters, segment table
       if (rc) return rc;
     }
+    // the scratch the large-k paths last asked for, allocated once for the
+    // next ones (the device is done with the old arena: its last search is)
+    if (h->arena.need > h->arena.bytes) {
+      if (h->ws_done) HIP_TRY(hipEventSynchronize(h->ws_done), "hipEventSynchronize");
+      hipFree(h->arena.base);
+      h->arena.base = nullptr;
+      h->arena.bytes = 0;
+      HIP_TRY(hipMalloc((void**)&h->arena.base, h->arena.need), "hipMalloc(large-k scratch)");
+      h->arena.bytes = h->arena.need;
+    }
+    h->arena.used = 0;
+    h->ws.arena = &h->arena;
     HIP_TRY(order_ws(h, st), "workspace order");
     // this search selects without the counters: the stats read as zero, not
     // as the previous search's
@@ -401,7 +414,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
       h->large_fallback = nfb;
     } else {
       h->large_fallback = -1;
-      HIP_TRY(launch_search_large(h->ix, d_queries, Q, T, k, d_docs, d_scores, st),
+      HIP_TRY(launch_search_large(h->ix, d_queries, Q, T, k, d_docs, d_scores, st, &h->arena),
               "large-k search launch");
     }
     if (ev) {
@@ -637,6 +650,7 @@ int bm25_index_destroy(bm25_index* h) {
   }
   if (h->ws_done) hipEventDestroy(h->ws_done);
   free_ws(h->ws);
+  hipFree(h->arena.base);
   hipFree(h->d_q);
   hipFree(h->d_docs);
   hipFree(h->d_scores);

@@ -140,8 +140,21 @@ struct DevIndex {
 
 constexpr int kCounters = 8;  // Workspace::counters
 
+// A handle's reusable scratch for the large-k paths (bm25mi_large.hip): one
+// device allocation, bump-allocated by each search (nested uses stack), sized
+// by the host before a search to what the last searches asked for — so a
+// search makes no allocation of its own once the handle has seen its shape.
+struct LargeArena {
+  char* base = nullptr;
+  size_t bytes = 0;
+  size_t used = 0;     // bump offset of the live scratch users
+  size_t need = 0;     // the most the last searches asked for
+  int64_t budget = 0;  // bytes one search may take (large_budget(), fixed at first use)
+};
+
 struct Workspace {
   int64_t cap_q = 0, cap_k = 0;
+  LargeArena* arena = nullptr;   // the handle's large-k scratch (null: per-search allocations)
   uint64_t* cand = nullptr;      // [Q][ntiles][kTileM] exact top-kTileM keys of sample (or all) tiles
   uint64_t* theta = nullptr;     // [Q] k-th best sample key
   uint64_t* list = nullptr;      // [Q][list_cap] keys above theta of the other tiles
@@ -263,7 +276,8 @@ hipError_t launch_scores_batch(const DevIndex& ix, const int32_t* d_queries, int
 // stream-ordered (hipMallocAsync) and released at the end of the launch
 // sequence.
 hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
-                               int k, int32_t* d_docs, float* d_scores, hipStream_t stream);
+                               int k, int32_t* d_docs, float* d_scores, hipStream_t stream,
+                               LargeArena* arena = nullptr);
 // The large-k list path's passes (bm25mi_kernels.hip; used by
 // bm25mi_large.hip): SAMPLE with kLargeM keys per sample tile into keys[Q][g.S]
 // (g.m == kLargeM), and REST into the workspace's theta / list / list_cnt /

@@ -406,21 +406,60 @@ int64_t large_budget() {
 }
 
 // Stream-ordered scratch: released on `st` after everything enqueued so far.
+// The device's default pool keeps what is released (release threshold: no
+// limit) — with the default threshold of 0 every synchronisation handed the
+// pool's pages back, and the next search of the path (which synchronises
+// once) mapped its ~2 GB of scratch again.  At most large_budget() bytes at a
+// time; PyTorch's caching allocator does not draw on this pool.
+// With a handle's arena (LargeArena) the buffers come from it, and what does
+// not fit is allocated and counted, so the host grows the arena before the
+// handle's next search: a large-k search then allocates nothing (each
+// stream-ordered allocation and free cost the host ~0.1 ms: ~2 ms per search
+// at c3, k = 10 000, before its first kernel).
 struct Scratch {
   hipStream_t st;
   std::vector<void*> ptrs;
-  explicit Scratch(hipStream_t s) : st(s) {}
+  LargeArena* ar;
+  size_t start, total = 0;
+  explicit Scratch(hipStream_t s, LargeArena* a = nullptr)
+      : st(s), ar(a), start(a ? a->used : 0) {
+    int dev = 0;
+    hipMemPool_t pool = nullptr;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   template <class T>
   hipError_t get(T** p, int64_t n) {
     *p = nullptr;
-    const hipError_t e = hipMallocAsync((void**)p, sizeof(T) * (size_t)std::max<int64_t>(n, 1), st);
+    const size_t size = (sizeof(T) * (size_t)std::max<int64_t>(n, 1) + 255) & ~(size_t)255;
+    total += size;
+    if (ar && ar->base && ar->used + size <= ar->bytes) {
+      *p = reinterpret_cast<T*>(ar->base + ar->used);
+      ar->used += size;
+      return hipSuccess;
+    }
+    const hipError_t e = hipMallocAsync((void**)p, size, st);
     if (e == hipSuccess) ptrs.push_back((void*)*p);
     return e;
   }
   ~Scratch() {
+    if (ar) {
+      ar->need = std::max(ar->need, start + total);
+      ar->used = start;
+    }
     for (void* p : ptrs) hipFreeAsync(p, st);
   }
 };
+
+// The byte budget of one large-k launch sequence: the arena's, fixed at its
+// first use (hipMemGetInfo costs the host too), else the device's free memory.
+int64_t budget_of(LargeArena* ar) {
+  if (!ar) return large_budget();
+  if (ar->budget == 0) ar->budget = large_budget();
+  return ar->budget;
+}
 
 #define LK_TRY(expr)                    \
   do {                                  \
@@ -435,7 +474,8 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
 }  // namespace
 
 hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
-                               int k, int32_t* d_docs, float* d_scores, hipStream_t st) {
+                               int k, int32_t* d_docs, float* d_scores, hipStream_t st,
+                               LargeArena* arena) {
   if (Q == 0 || k == 0) return hipSuccess;
   ix.disp.kernels |= kKLarge;
   const int kv = (int)std::min<int64_t>(k, ix.n_docs);  // a doc shard may hold fewer than k
@@ -445,11 +485,11 @@ hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int
   }
   const int64_t Np = ix.ntiles << ix.tile_shift;  // row stride: whole tiles
   const int64_t per_q = Np * 4 + (int64_t)kv * 16 + 256 * 4 + 64 + sort_bytes(1, kv);
-  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));
+  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, budget_of(arena) / per_q));
   G = std::min<int64_t>(G, 65535);
   G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / kv - 1));
   const int64_t sb = sort_bytes(G, kv);
-  Scratch sc(st);
+  Scratch sc(st, arena);
   float* scores = nullptr;
   uint32_t* hist = nullptr;
   SelState* state = nullptr;
@@ -813,9 +853,9 @@ hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_querie
   const int64_t Co = std::max<int64_t>(1, C / 2);
   const int64_t per_q = (g.S + C + 2 * (int64_t)k + ix.ntiles * Cb + Co) * 8 + ix.ntiles * 4 +
                         64 + 8 * (int64_t)k + (int64_t)radix_sort_scratch_bytes(k) + 64;
-  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, large_budget() / per_q));
+  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, budget_of(ws.arena) / per_q));
   G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / C - 1));
-  Scratch sc(st);
+  Scratch sc(st, ws.arena);
   uint64_t *skeys = nullptr, *theta = nullptr, *list = nullptr, *kth = nullptr, *keys = nullptr,
            *alt = nullptr, *slots = nullptr, *ovf = nullptr;
   int32_t *cnt = nullptr, *fb = nullptr, *slot_cnt = nullptr;
@@ -885,7 +925,7 @@ hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_querie
   if (T > 0)
     hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(nf * T, 256, 4096)), dim3(256), 0, st,
                        d_queries, d_ids, nf, T, fq);
-  LK_TRY(launch_search_large(ix, fq, nf, T, k, fd, fs, st));
+  LK_TRY(launch_search_large(ix, fq, nf, T, k, fd, fs, st, ws.arena));
   hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for(nf * k, 256, 4096)), dim3(256), 0, st, fd,
                      fs, d_ids, nf, (int64_t)k, d_docs, d_scores);
   // (ids lives on the host until the copy above has run)
