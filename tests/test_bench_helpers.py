@@ -23,8 +23,11 @@ def test_traffic_entries_match_their_workload():
         assert t["hbm_bytes_per_launch"] > 0
         assert 0.0 < t["l2_hit_rate"] < 1.0 and t["method"] and t["source"]
         seen[(config, terms)] = t["hbm_bytes_per_launch"]
-    # 16-term queries read about twice the postings of 8-term ones
-    assert seen[("c3", 16)] > 1.5 * seen[("c3", 8)]
+    # 16-term queries read about twice the postings of 8-term ones (more of
+    # them L2 hits: the moved bytes grow less), and every entry stays below
+    # its workload's algorithmic bytes (17.9 GB at 8 terms, 34.7 GB at 16)
+    assert seen[("c3", 16)] > 1.2 * seen[("c3", 8)]
+    assert seen[("c3", 8)] < 17.9e9 and seen[("c3", 16)] < 34.7e9
     assert bench.load_traffic(path, "c3", 12, 8) is None  # other tile size
     assert bench.load_traffic(path, "c2", 11, 8) is None  # never profiled
 
