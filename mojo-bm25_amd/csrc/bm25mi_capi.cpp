@@ -247,6 +247,11 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMalloc(wctr)");
   // claim counters start at 0; each flat launch's last wave re-zeroes its region
   HIP_TRY(hipMemset(ws.wctr, 0, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMemset(wctr)");
+  // both memsets ran on the null stream, which a non-blocking search stream
+  // (torch's, the handle's own) does not wait for: complete them before the
+  // first kernel reads the counters (a fork's first search in a part stream
+  // once read a half-zeroed claim counter and skipped items)
+  HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize(null)");
   ws.cap_seg = need_seg;
   if (ws.cap_seg > 0) HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * ws.cap_seg), "hipMalloc(seg)");
   ws.list_cap = C;
