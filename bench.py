@@ -313,10 +313,12 @@ def main():
     prof = index.profile_read()
     dispatch = index.last_dispatch()
     stats = index.search_stats()  # the last timed search's selection counters
-    if info.get("tile_bounds"):
+    if info.get("tile_bounds") and (world == 1 or replica):
         # the (query, tile) pairs the tile bound skipped and their postings:
         # counted by the count_skips REST build (registers the timed build does
         # without), in one extra search of the same batch after the timed ones
+        # (not in a doc-sharded run: its search is collective, and the extra
+        # one must not depend on a rank's own index)
         index.set_option("count_skips", 1)
         step()
         torch.cuda.synchronize(dev)
