@@ -677,10 +677,13 @@ __device__ __forceinline__ void emit_rest_slot(float* acc, int64_t tile, int64_t
 }
 
 // The large-k list path's REST tiles with a crossing list: the row loop has
-// recorded (xl, n of them) the slot of every document whose running sum
-// reached theta's score — once per document: sums only grow — so only those
-// are tested and keyed, into the tile's slot as emit_rest_slot does, instead
-// of a pass over the tile's 2048 accumulators.
+// recorded (xl, n of them) the slot of a document each time one of its adds
+// left its sum at or above theta's score — a document more than once when it
+// gets postings after crossing — so only those are tested and keyed, into the
+// tile's slot as emit_rest_slot does, instead of a pass over the tile's 2048
+// accumulators.  Each entry takes its accumulator by an LDS exchange with -1
+// (sums are >= 0 on a non-negative index): only a document's first entry
+// gets its sum, the others read -1 and pass nothing.
 constexpr int kCrossCap = 256;  // crossing-list entries per wave (512 B of LDS)
 template <int S>
 __device__ __forceinline__ void emit_cross(float* acc, const uint16_t* xl, int32_t nx,
@@ -701,8 +704,8 @@ __device__ __forceinline__ void emit_cross(float* acc, const uint16_t* xl, int32
     const int32_t i = i0 + (int32_t)lane;
     const uint32_t off = i < nx ? (uint32_t)xl[i] : 0u;
     const int d = (int)(off >> 2);
-    const float f = acc[d];
-    const bool pass = i < nx && d < lim && ((f > th) | ((f == th) & (d < tie)));
+    const float f = i < nx ? atomicExch(&acc[d], -1.0f) : -1.0f;  // (first entry: the sum)
+    const bool pass = i < nx && f >= 0.f && d < lim && ((f > th) | ((f == th) & (d < tie)));
     const uint64_t m = __ballot(pass);
     if (m == 0ull) continue;
     const int32_t tot = (int32_t)__popcll(m);
@@ -1517,9 +1520,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const float y0 = xc0 + ac0, y1 = xc1 + ac1;
     lds_at(sc0) = y0;
     lds_at(sc1) = y1;
-    if constexpr (kCross) {  // a doc whose sum reaches theta's score now (trash lanes: -inf)
-      const uint64_t m0 = __ballot((y0 >= thS) & (xc0 < thS));
-      const uint64_t m1 = __ballot((y1 >= thS) & (xc1 < thS));
+    if constexpr (kCross) {  // a doc whose sum is at or above theta's score (trash lanes: -inf);
+      // one compare per slot: a doc that is already above records again, and
+      // emit_cross keeps its first entry
+      const uint64_t m0 = __ballot(y0 >= thS);
+      const uint64_t m1 = __ballot(y1 >= thS);
       if ((m0 | m1) != 0ull) {
         const int32_t n0 = (int32_t)__popcll(m0), n1 = (int32_t)__popcll(m1);
         if (ncross + n0 + n1 <= kCrossCap) {
