@@ -30,7 +30,8 @@ constants are stated in the output line.  Two ways to add them:
       PROBE_GRID: grid_pct values, e.g. "100,90"; PROBE_HYBRID=1: also the
       2-replica x W/2-shard split, each rank Q/2 queries on a 2/W shard;
       PROBE_PIPE=2: two batches in flight per rank, on the handle and a fork
-      with their own streams, collectives inline on one comm stream)
+      with their own streams, collectives inline on one comm stream;
+      PROBE_LOCAL=1: each shard's own single-index top-k, one all-gather)
 """
 import json
 import os
@@ -249,6 +250,21 @@ def main():
                                 forks[r] = [shards[r].fork() for _ in rows[1:]]
                             rank_parts(shards, r, q, k, W, smax, keys_p, g_p, rows, out_d,
                                        out_s, forks[r], streams, comm, kus, lus)
+                    elif os.environ.get("PROBE_LOCAL") == "1":
+                        # local threshold: each shard's own top-k (its single-index
+                        # search), one all-gather of the lists, the W-way merge
+                        for r, ix_ in enumerate(shards):
+                            ix_.search_device(q, k, g_p[0][r, 0], g_p[0][r, 1].view(torch.float32),
+                                              st)
+                        torch.cuda.synchronize()
+
+                        def one(r):
+                            ix_ = shards[r]
+                            ix_.search_device(q, k, g_p[0][r, 0], g_p[0][r, 1].view(torch.float32),
+                                              st)
+                            merge_sorted_device(q.device.index, g_p[0],
+                                                g_p[0][:, 1].view(torch.float32), W, Q, k,
+                                                2 * Q * k, out_d, out_s, st)
                     else:
                         def one(r):
                             ix_ = shards[r]
@@ -274,7 +290,9 @@ def main():
                                      "fallback_queries": shards[r].search_stats()["fallback_queries"]})
                 worst = max(x["ms"] for x in per_rank)
                 inline = inline or pipe > 1
-                coll_us = 0.0 if inline else (model_gather_us(keys_b, W) + model_gather_us(list_b, W))
+                coll_us = 0.0 if inline else (model_gather_us(list_b, W) if
+                                              os.environ.get("PROBE_LOCAL") == "1" else
+                                              model_gather_us(keys_b, W) + model_gather_us(list_b, W))
                 proj = worst + coll_us * 1e-3
                 if W == 1 and P == 1 and R == 1 and gp == 100:
                     w1_ms = worst
