@@ -163,6 +163,27 @@ def cpu_baseline(args, n_docs, indptr, indices, data, queries, k):
                                      "note": f"EXTRAPOLATION: sample time x {Q}/sample"}}
 
 
+def launch_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) run without a launcher: start the N ranks as a
+    child torch.distributed.run on 127.0.0.1 (this process has not touched
+    the GPU and is not replaced: it waits for the child and returns its exit
+    status), so the line reports n_gpus = N or the run fails — never a
+    silent one-GPU measurement."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n} without WORLD_SIZE: launching {n} ranks: {' '.join(cmd)}")
+    rc = subprocess.run(cmd).returncode
+    if rc != 0:
+        log(f"[bench] the {n}-rank run failed (exit status {rc})")
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -206,6 +227,8 @@ def main():
                     help="replica mode at N=1: run rank 0's slice of an R-way replica job "
                          "(Q/R queries on the whole index) — the one-GPU proxy of the N=R line")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     if args.replica_of > 1:
         args.mode = "replica"
 
@@ -218,7 +241,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch "
+                         f"--nproc-per-node {args.gpus}, or pass --gpus {world}")
     cfg = synth.CONFIGS[args.config]
     import dataclasses
     if args.terms > 0:

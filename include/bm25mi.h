@@ -336,7 +336,7 @@ int bm25_search_stats_ex(bm25_index* idx, int64_t* rescored_tiles,
  *   [4] queries left to
  *   the block merge (lists longer than one wavefront's registers), [5] k >
  *   4096: queries the list path handed to dense score rows (-1: the dense
- *   path served the whole search).
+ *   path served the whole search; 0 after a search of k <= 4096).
  * n must be in 1..6. */
 int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
 

@@ -83,6 +83,12 @@ class GpuIndex:
 
     # ------------------------------------------------------------------
     def close(self) -> None:
+        """Destroy the handle and every fork bm25mi.dist cached on it.  The
+        device arrays are shared (bm25_index_fork), so they are released only
+        when the last of those handles is gone."""
+        for f in self.__dict__.pop("_bm25_forks", []):
+            f.close()
+        self.__dict__.pop("_bm25_part_streams", None)
         if self._h is not None:
             lib.bm25_index_destroy(self._h)
             self._h = None

@@ -213,7 +213,13 @@ int get_opt(const SearchOpts& o, const char* name, int64_t* v) {
   return BM25_OK;
 }
 
-int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
+// The workspace for a search of Q queries of T terms at k, enqueued on st.
+// A (re)allocated workspace's counters are zeroed on st itself, so they are
+// ordered before the search's first kernel on any stream, blocking or not
+// (they were zeroed on the null stream once, which a non-blocking stream does
+// not wait for: a fork's first search on a part stream read a half-zeroed
+// claim counter and skipped items).
+int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k, hipStream_t st) {
   Workspace& ws = h->ws;
   const int64_t need_seg = seg_entries(h->ix, std::max(Q, ws.cap_q), T);
   if (Q <= ws.cap_q && k <= ws.cap_k) {
@@ -242,16 +248,12 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k) {
   HIP_TRY(hipMalloc(&ws.nflag, sizeof(int32_t) * q), "hipMalloc(nflag)");
   HIP_TRY(hipMalloc(&ws.queue, sizeof(int32_t) * q * mf), "hipMalloc(queue)");
   HIP_TRY(hipMalloc(&ws.counters, sizeof(int32_t) * kCounters), "hipMalloc(counters)");
-  HIP_TRY(hipMemset(ws.counters, 0, sizeof(int32_t) * kCounters), "hipMemset(counters)");
+  HIP_TRY(hipMemsetAsync(ws.counters, 0, sizeof(int32_t) * kCounters, st), "hipMemsetAsync(counters)");
   HIP_TRY(hipMalloc(&ws.slow, sizeof(int32_t) * q), "hipMalloc(slow)");
   HIP_TRY(hipMalloc(&ws.wctr, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMalloc(wctr)");
   // claim counters start at 0; each flat launch's last wave re-zeroes its region
-  HIP_TRY(hipMemset(ws.wctr, 0, sizeof(int32_t) * kWctrRegions * kWctrInts), "hipMemset(wctr)");
-  // both memsets ran on the null stream, which a non-blocking search stream
-  // (torch's, the handle's own) does not wait for: complete them before the
-  // first kernel reads the counters (a fork's first search in a part stream
-  // once read a half-zeroed claim counter and skipped items)
-  HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize(null)");
+  HIP_TRY(hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrRegions * kWctrInts, st),
+          "hipMemsetAsync(wctr)");
   ws.cap_seg = need_seg;
   if (ws.cap_seg > 0) HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * ws.cap_seg), "hipMalloc(seg)");
   ws.list_cap = C;
@@ -388,7 +390,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
     const bool lists = h->ix.opt.large_lists && k <= kLargeListMaxK && k <= h->ix.n_docs &&
                        large_list_supported(h->ix, T, Q) && large_geom(h->ix, k).P > 0;
     if (lists) {
-      const int rc = ensure_ws(h, Q, T, 1);  // claim counters, counters, segment table
+      const int rc = ensure_ws(h, Q, T, 1, st);  // claim counters, counters, segment table
       if (rc) return rc;
     }
     // the scratch the large-k paths last asked for, allocated once for the
@@ -433,9 +435,10 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
     }
     return BM25_OK;
   }
-  int rc = ensure_ws(h, Q, T, k);
+  int rc = ensure_ws(h, Q, T, k, st);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
+  h->large_fallback = 0;  // (counter [5] belongs to the last search: no large-k rows here)
   choose_theta_source(h);
   const int P = search_geom(h->ix, h->ix.ntiles, k, 1, T).P;
   h->ix.disp = Dispatch{};
@@ -808,10 +811,11 @@ int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   if (Q == 0 || k == 0 || k > kMaxK) return BM25_OK;  // k > kMaxK: no sample half
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
-  rc = ensure_ws(h, Q, T, k);
-  if (rc) return rc;
   const hipStream_t st = (hipStream_t)stream;
+  rc = ensure_ws(h, Q, T, k, st);
+  if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
+  h->large_fallback = 0;
   h->split_ev = next_events(h);
   if (h->split_ev) HIP_TRY(hipEventRecord(h->split_ev->a, st), "hipEventRecord");
   choose_theta_source(h);  // (the finish half keeps this choice)
@@ -840,9 +844,10 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
     h->sampled = false;
     return run_search(h, d_queries, Q, T, k, d_docs, d_scores, st);
   }
-  rc = ensure_ws(h, Q, T, k);
+  rc = ensure_ws(h, Q, T, k, st);
   if (rc) return rc;
   HIP_TRY(order_ws(h, st), "workspace order");
+  h->large_fallback = 0;
   if (!h->sampled) choose_theta_source(h);  // no sample half ran for this search (S = 0)
   const SampleGeom g = shard_geom(h, shard_docs_max, world, k, T);
   if (!h->sampled) {

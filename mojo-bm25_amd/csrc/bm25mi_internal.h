@@ -272,12 +272,14 @@ hipError_t launch_scores_batch(const DevIndex& ix, const int32_t* d_queries, int
 // Exact top-k for any k (the path of k > kMaxK, bm25mi_large.hip): per chunk
 // of queries the dense scores, a radix selection of the k-th key, the keys
 // >= it compacted and sorted.  k > n_docs (a doc shard smaller than k) pads
-// each row with doc -1 / score bits 0xFFFFFFFF.  Device memory is taken
-// stream-ordered (hipMallocAsync) and released at the end of the launch
-// sequence.
+// each row with doc -1 / score bits 0xFFFFFFFF.  Scratch comes from the
+// handle's arena; what does not fit is taken stream-ordered (hipMallocAsync)
+// and released at the end of the launch sequence.  budget: the bytes this
+// call may take (<= 0: the arena's budget; a nested call passes what its
+// caller leaves).
 hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                                int k, int32_t* d_docs, float* d_scores, hipStream_t stream,
-                               LargeArena* arena = nullptr);
+                               LargeArena* arena = nullptr, int64_t budget = 0);
 // The large-k list path's passes (bm25mi_kernels.hip; used by
 // bm25mi_large.hip): SAMPLE with kLargeM keys per sample tile into keys[Q][g.S]
 // (g.m == kLargeM), and REST into the workspace's theta / list / list_cnt /

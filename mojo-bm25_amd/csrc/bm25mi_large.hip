@@ -405,31 +405,25 @@ int64_t large_budget() {
   return std::max<int64_t>(64ll << 20, std::min<int64_t>((int64_t)free_b / 4, 4ll << 30));
 }
 
-// Stream-ordered scratch: released on `st` after everything enqueued so far.
-// The device's default pool keeps what is released (release threshold: no
-// limit) — with the default threshold of 0 every synchronisation handed the
-// pool's pages back, and the next search of the path (which synchronises
-// once) mapped its ~2 GB of scratch again.  At most large_budget() bytes at a
-// time; PyTorch's caching allocator does not draw on this pool.
-// With a handle's arena (LargeArena) the buffers come from it, and what does
-// not fit is allocated and counted, so the host grows the arena before the
-// handle's next search: a large-k search then allocates nothing (each
-// stream-ordered allocation and free cost the host ~0.1 ms: ~2 ms per search
-// at c3, k = 10 000, before its first kernel).
+// Scratch of one launch sequence.  With a handle's arena (LargeArena) the
+// buffers come from it; what does not fit is allocated stream-ordered,
+// released on `st` after everything enqueued so far, and counted, so the host
+// grows the arena before the handle's next search: a large-k search then
+// allocates nothing (each stream-ordered allocation and free cost the host
+// ~0.1 ms: ~2 ms per search at c3, k = 10 000, before its first kernel).  The
+// device's default pool keeps its default release threshold (the process's
+// other users of the pool are not affected); what a handle retains is its
+// arena, at most its budget (large_budget at first use), plus what the first
+// search allocated stream-ordered until the pool trims it at a
+// synchronisation.  At most budget bytes at a time: a nested launch sequence
+// (the list path's dense rows) gets what its caller's scratch leaves.
 struct Scratch {
   hipStream_t st;
   std::vector<void*> ptrs;
   LargeArena* ar;
   size_t start, total = 0;
   explicit Scratch(hipStream_t s, LargeArena* a = nullptr)
-      : st(s), ar(a), start(a ? a->used : 0) {
-    int dev = 0;
-    hipMemPool_t pool = nullptr;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-      uint64_t keep = UINT64_MAX;
-      hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
-  }
+      : st(s), ar(a), start(a ? a->used : 0) {}
   template <class T>
   hipError_t get(T** p, int64_t n) {
     *p = nullptr;
@@ -475,7 +469,7 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
 
 hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                                int k, int32_t* d_docs, float* d_scores, hipStream_t st,
-                               LargeArena* arena) {
+                               LargeArena* arena, int64_t budget) {
   if (Q == 0 || k == 0) return hipSuccess;
   ix.disp.kernels |= kKLarge;
   const int kv = (int)std::min<int64_t>(k, ix.n_docs);  // a doc shard may hold fewer than k
@@ -485,7 +479,8 @@ hipError_t launch_search_large(const DevIndex& ix, const int32_t* d_queries, int
   }
   const int64_t Np = ix.ntiles << ix.tile_shift;  // row stride: whole tiles
   const int64_t per_q = Np * 4 + (int64_t)kv * 16 + 256 * 4 + 64 + sort_bytes(1, kv);
-  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, budget_of(arena) / per_q));
+  if (budget <= 0) budget = budget_of(arena);
+  int64_t G = std::max<int64_t>(1, std::min<int64_t>(Q, budget / per_q));
   G = std::min<int64_t>(G, 65535);
   G = std::min<int64_t>(G, std::max<int64_t>(1, (int64_t)INT32_MAX / kv - 1));
   const int64_t sb = sort_bytes(G, kv);
@@ -925,7 +920,10 @@ hipError_t launch_search_large_lists(const DevIndex& ix, const int32_t* d_querie
   if (T > 0)
     hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(nf * T, 256, 4096)), dim3(256), 0, st,
                        d_queries, d_ids, nf, T, fq);
-  LK_TRY(launch_search_large(ix, fq, nf, T, k, fd, fs, st, ws.arena));
+  // the dense rows get what this sequence's scratch leaves of the budget
+  const int64_t left = budget_of(ws.arena) - (int64_t)sc.total;
+  LK_TRY(launch_search_large(ix, fq, nf, T, k, fd, fs, st, ws.arena,
+                             std::max<int64_t>(left, 64ll << 20)));
   hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for(nf * k, 256, 4096)), dim3(256), 0, st, fd,
                      fs, d_ids, nf, (int64_t)k, d_docs, d_scores);
   // (ids lives on the host until the copy above has run)

@@ -59,3 +59,33 @@ def test_posting_counts_per_query_and_batch_distinct():
     assert bench.query_postings(indptr, q) == 14
     assert bench.batch_distinct_postings(indptr, q) == 8
     assert bench.batch_distinct_postings(indptr, np.full((2, 3), -1, np.int32)) == 0
+
+
+def test_gpus_n_without_launcher_launches_ranks():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts the
+    two ranks itself (a child torch.distributed.run on 127.0.0.1): the line
+    reports n_gpus 2, or — here, with no GPU — the run fails non-zero.  It
+    never silently measures one GPU."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--backend", "gloo", "--config", "c2", "--steps", "1", "--warmup", "0",
+                        "--cpu-queries", "0", "--e2e-batches", "0", "--threads", "4"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert "launching 2 ranks" in r.stderr, r.stderr[-2000:]
+    if r.returncode == 0:
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        assert line["n_gpus"] == 2
+    else:
+        assert r.returncode != 0
+
+
+def test_gpus_mismatch_with_world_size_fails():
+    """--gpus N under a launcher of another world size is an error, not a note."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--cpu-queries", "0"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr, r.stderr[-2000:]

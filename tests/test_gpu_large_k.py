@@ -212,6 +212,9 @@ def test_large_k_list_path(gpu, segments):
         index.set_option("large_lists", 0)
         _exact(index.search(q, k), ref)
         assert index.search_stats()["large_dense_queries"] == -1
+    # counter [5] belongs to the last search: a k <= 4096 search resets it
+    _exact(index.search(q, 100), oracle.search_c(cfg.n_docs, ip, ix, dt, q, 100, threads=8))
+    assert index.search_stats()["large_dense_queries"] == 0
     index.close()
 
 
@@ -244,3 +247,50 @@ def test_large_k_list_path_overflow_falls_back(gpu):
     _exact(index.search(q, k), ref)
     assert 1 <= index.search_stats()["large_dense_queries"] < len(q)
     index.close()
+
+
+def test_large_k_list_path_doc_shards(gpu):
+    """the list path on doc shards (doc_offset != 0) — the global
+    -> local threshold conversion of row_kth_kernel<0>, zero fill with local
+    ids and the offset added by row_sort_write_kernel.  Two 3M-doc shards of
+    a 6M-doc index at 4096 < k <= a shard's sample keys, an all-padding row
+    (zero fill) and a rare-term row: each shard's list-path top-k (no dense
+    rows), merged, is the single-index result bit for bit."""
+    import torch
+    from bm25mi import synth
+    from bm25mi.dist import sharded_search
+    from bm25mi.index import GpuIndex, merge_sorted_device
+    cfg = synth.Config("LS", 6_000_000, 20_000, 80_000_000, 12, 8, 4500)
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    q[0, :] = -1                                   # all padding: zero fill
+    q[1, :] = np.argsort(np.diff(ip))[:8]          # rare terms: fewer than k docs
+    W, Q = 2, len(q)
+    bounds = [synth.shard_bounds(cfg.n_docs, W, r) for r in range(W)]
+    sdm = max(hi - lo for lo, hi in bounds)
+    dq = torch.from_numpy(q).cuda()
+    st = torch.cuda.current_stream()
+
+    class Ex:
+        world = W
+
+        def __call__(self, keys):
+            return keys.unsqueeze(0).expand(W, *keys.shape).contiguous()
+
+    for k in (4097, 4500):
+        ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, k, threads=8)
+        g = torch.empty((W, 2, Q, k), dtype=torch.int32, device="cuda")
+        for r, (lo, hi) in enumerate(bounds):
+            sh = GpuIndex(*synth.make_index(cfg, lo, hi), hi - lo, doc_offset=lo)
+            sharded_search(sh, dq, k, sdm, g[r, 0], g[r, 1].view(torch.float32), None, st,
+                           exchange=Ex())
+            d = sh.last_dispatch()
+            assert {"large_k", "flat_sample", "flat_rest"} <= d["kernels"], d
+            assert sh.search_stats()["large_dense_queries"] == 0
+            torch.cuda.synchronize()
+            sh.close()
+        md = torch.empty((Q, k), dtype=torch.int32, device="cuda")
+        ms = torch.empty((Q, k), dtype=torch.float32, device="cuda")
+        merge_sorted_device(0, g, g[:, 1].view(torch.float32), W, Q, k, 2 * Q * k, md, ms, st)
+        torch.cuda.synchronize()
+        _exact((md.cpu().numpy(), ms.cpu().numpy()), ref)

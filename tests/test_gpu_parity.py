@@ -1358,3 +1358,105 @@ def test_fork_shares_arrays_concurrent_streams(gpu):
     base.close()  # the fork keeps the arrays
     _exact(fork.search(q, cfg.k), ref)
     fork.close()
+
+
+# ------------------------------------------------- round 6: stream order, close
+def test_fork_first_search_fresh_stream_reallocates(gpu):
+    """a (re)allocated workspace's claim counters are zeroed
+    on the search's own stream, not on the null stream a non-blocking stream
+    does not wait for.  A fresh fork's first search on a new non-blocking
+    torch stream — and later searches on new streams with batches that force
+    the workspace to grow — give the oracle's bits."""
+    import torch
+    from bm25mi import synth
+    cfg = synth.Config("fs", 900_000, 4000, 7_000_000, 200, 8, 40)
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k)
+    base = _idx(ip, ix, dt, cfg.n_docs)
+    dq = torch.from_numpy(q).cuda()
+    d = torch.empty((len(q), cfg.k), dtype=torch.int32, device="cuda")
+    s = torch.empty((len(q), cfg.k), dtype=torch.float32, device="cuda")
+    base.search_device(dq[:8], cfg.k, d[:8], s[:8], torch.cuda.Stream())
+    torch.cuda.synchronize()
+    for rows in (16, 64, len(q)):  # each a larger batch: the fork's workspace grows
+        fork = base.fork()
+        st = torch.cuda.Stream()
+        assert st.query()  # a new non-blocking stream with nothing on it
+        fork.search_device(dq[:rows], cfg.k, d[:rows], s[:rows], st)
+        grow = base.fork()
+        st2 = torch.cuda.Stream()
+        grow.search_device(dq[:4], cfg.k, d[:4], s[:4], st2)
+        grow.search_device(dq[:rows], cfg.k, d[:rows], s[:rows], st2)  # reallocates on st2
+        torch.cuda.synchronize()
+        _exact((d[:rows].cpu().numpy(), s[:rows].cpu().numpy()), (ref[0][:rows], ref[1][:rows]))
+        fork.close()
+        grow.close()
+    base.close()
+
+
+def test_close_releases_cached_forks(gpu):
+    """GpuIndex.close() also closes the forks bm25mi.dist caches on
+    the index (parts > 1), so the shared device arrays and every fork's
+    workspace are released at close, not at garbage collection."""
+    import gc
+    import torch
+    from bm25mi import synth
+    from bm25mi.dist import _forks
+    cfg = synth.Config("cl", 2_000_000, 5000, 30_000_000, 64, 8, 10)
+    ip, ix, dt = synth.make_index(cfg)
+    q = synth.make_queries(cfg)
+    torch.cuda.synchronize()
+    gc.collect()
+    free0 = torch.cuda.mem_get_info()[0]
+    index = _idx(ip, ix, dt, cfg.n_docs)
+    ctxs = _forks(index, 3)
+    assert len(ctxs) == 3 and index._bm25_forks
+    for c in ctxs:
+        c.search(q, cfg.k)
+    held = free0 - torch.cuda.mem_get_info()[0]
+    assert held > 200 << 20, held  # the index arrays (~300 MB) and three workspaces
+    index.close()
+    assert "_bm25_forks" not in index.__dict__ and all(c._h is None for c in ctxs)
+    torch.cuda.synchronize()
+    left = free0 - torch.cuda.mem_get_info()[0]
+    assert left < 16 << 20, (held, left)
+
+
+def test_gpu_execute_query_realistic_matrix(gpu):
+    """gpu_execute_query (gpu_bm25/common.py:28-85) fed as
+    the reference's driver feeds it (main.py:238-252) — bm25.py's fitted dense
+    matrix cast to f32 (bm25_dense.npz, generated by the reference itself),
+    query vectors from term_to_id with OOV terms mapped to id 0 — plus
+    duplicate ids, negative ids (normalised as MAX gather does) and a
+    corpus-sized sparse-ish dense matrix.  The top-1 index / weight match the
+    oracle's top-1 on the same fp32 columns in query order.  Parity with MAX
+    itself is unpinned (MAX is not importable here)."""
+    import scipy.sparse as sp
+    from gpu_bm25.common import gpu_execute_query
+    g = _load("bm25_dense.npz")
+    m = g["bm25_matrix"].astype(np.float32)
+    term_to_id = {t: i for i, t in enumerate(g["vocabulary"].tolist())}
+    cases = [[term_to_id.get(t, 0) for t in str(qs).lower().split()] for qs in g["queries"]]
+    cases += [[term_to_id["fox"]] * 3 + [term_to_id["dog"]], [-1, 0, -2], [0, 0, 0, 0]]
+
+    def check(mat, qv):
+        qv = np.asarray(qv, np.int32)
+        idx, w = gpu_execute_query(mat, qv, None, None)
+        assert idx.shape == (1, 1) and idx.dtype == np.int64 and w.dtype == np.float32
+        norm = np.where(qv < 0, qv + mat.shape[1], qv).astype(np.int32)
+        c = sp.csc_matrix(mat)
+        rd, rs = oracle.search_c(mat.shape[0], c.indptr, c.indices, c.data, norm[None, :], 1)
+        assert idx.item() == int(rd[0, 0]) and w.view(np.uint32).item() == rs.view(np.uint32)[0, 0], \
+            (qv, idx, w, rd, rs)
+
+    for qv in cases:
+        check(m, qv)
+    rng = np.random.default_rng(66)
+    big = rng.uniform(0.0, 4.0, (50_000, 300)).astype(np.float32)
+    big[rng.random(big.shape) < 0.9] = 0.0
+    for _ in range(4):
+        qv = rng.integers(0, 300, size=6)
+        qv[rng.random(6) < 0.3] = 0  # OOV -> 0
+        check(big, qv)
+    check(big, [17, 17, -300, -1])
