@@ -270,6 +270,21 @@ int bm25_search_finish_device(bm25_index* idx, const int32_t* d_queries, int64_t
                               int32_t k, int32_t world, int64_t shard_docs_max,
                               const uint64_t* d_all_keys, int32_t* d_docs, float* d_scores,
                               void* stream);
+/*
+ * The finish half on three streams, for a caller that pipelines batches
+ * (bm25mi.dist.ShardPipeline): theta on stream_theta, the REST pass on
+ * stream_rest (after theta), the merges into d_docs / d_scores on
+ * stream_select (after REST); the library orders the three with events.
+ * The workspace is released on stream_select: the handle's next search on
+ * another stream waits for it.  Same results as bm25_search_finish_device
+ * (which is this with one stream).  The score pass of a profiled handle is
+ * timed on stream_rest from the REST pass's start.
+ */
+int bm25_search_finish_streams_device(bm25_index* idx, const int32_t* d_queries, int64_t Q,
+                                      int64_t T, int32_t k, int32_t world,
+                                      int64_t shard_docs_max, const uint64_t* d_all_keys,
+                                      int32_t* d_docs, float* d_scores, void* stream_theta,
+                                      void* stream_rest, void* stream_select);
 
 /*
  * Doc-sharded index over several devices of ONE process.

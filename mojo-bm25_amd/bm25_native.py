@@ -12,8 +12,12 @@ Deliberate differences:
   * documents with equal scores are ordered by doc id ascending (the
     reference's order is numpy-implementation-defined, bm25_native.py:205-212).
 Every top_k <= num_docs is served, as by the reference's argpartition
-(bm25_native.py:204-214): k <= 4096 by the sampled-threshold pipeline, larger
-k by the exact dense-score radix selection (csrc/bm25mi_large.hip).
+(bm25_native.py:204-214): k <= 4096 by the thresholded pipeline (tile-bound or
+sampled threshold, REST lists, wave merges), larger k by the large-k list path
+of csrc/bm25mi_large.hip (sampled slice-maximum threshold, REST crossing
+lists, selection and row sort), and by dense score rows with a radix
+selection only where lists cannot serve (signed indices, k > 131 072, a list
+past its capacity).
 """
 from __future__ import annotations
 

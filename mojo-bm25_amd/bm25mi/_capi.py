@@ -81,6 +81,8 @@ _SIGS = {
     "bm25_sharded_destroy": ([_P], ctypes.c_int),
     "bm25_sample_width": ([_P, _I64, _I32, _I32, _PI64], ctypes.c_int),
     "bm25_search_sample_device": ([_P, _P, _I64, _I64, _I32, _I32, _I64, _P, _P], ctypes.c_int),
+    "bm25_search_finish_streams_device": ([_P, _P, _I64, _I64, _I32, _I32, _I64, _P, _P, _P, _P,
+                                           _P, _P], ctypes.c_int),
     "bm25_search_finish_device": ([_P, _P, _I64, _I64, _I32, _I32, _I64, _P, _P, _P, _P],
                                   ctypes.c_int),
     "bm25_build_scores": ([ctypes.c_int, _I64, _I64, _I64, _P, _P, _P, _P, ctypes.c_double,

@@ -187,6 +187,19 @@ class GpuIndex:
                                             ctypes.c_void_p(d_scores.data_ptr()),
                                             ctypes.c_void_p(s)))
 
+    def search_finish_streams_device(self, d_queries, k: int, world: int, shard_docs_max: int,
+                                     d_all_keys, d_docs, d_scores, stream_theta, stream_rest,
+                                     stream_select) -> None:
+        """search_finish_device on three streams (bm25_search_finish_streams_
+        device): theta, the REST pass and the merges, ordered by events."""
+        Q, T = d_queries.shape
+        ss = [getattr(x, "cuda_stream", x) or 0 for x in (stream_theta, stream_rest, stream_select)]
+        check(lib.bm25_search_finish_streams_device(
+            self._h, ctypes.c_void_p(d_queries.data_ptr()), Q, T, int(k), int(world),
+            int(shard_docs_max), ctypes.c_void_p(d_all_keys.data_ptr()),
+            ctypes.c_void_p(d_docs.data_ptr()), ctypes.c_void_p(d_scores.data_ptr()),
+            *[ctypes.c_void_p(x) for x in ss]))
+
     def scores_dense(self, query) -> np.ndarray:
         """All n_docs fp32 scores of one query (zero for untouched docs)."""
         q = np.ascontiguousarray(np.asarray(query).ravel(), dtype=np.int32)

@@ -88,6 +88,7 @@ struct bm25_index {
   int64_t device_bytes = 0;
   EventPair* split_ev = nullptr;  // events of a sample/finish search in flight
   hipEvent_t ws_done = nullptr;    // end of the last search that used the workspace
+  hipEvent_t ev_split[2] = {nullptr, nullptr};  // theta -> REST, REST -> select (three streams)
   hipStream_t ws_stream = nullptr; // its stream
   int32_t* d_maxtok = nullptr;     // bm25_max_token_device result
   bool sampled = false;            // a sample half ran since the last finish half
@@ -657,6 +658,8 @@ int bm25_index_destroy(bm25_index* h) {
     hipEventDestroy(p.c);
   }
   if (h->ws_done) hipEventDestroy(h->ws_done);
+  for (hipEvent_t e : h->ev_split)
+    if (e) hipEventDestroy(e);
   free_ws(h->ws);
   hipFree(h->arena.base);
   hipFree(h->d_q);
@@ -828,10 +831,13 @@ int bm25_search_sample_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   return BM25_OK;
 }
 
-int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T,
-                              int32_t k, int32_t world, int64_t shard_docs_max,
-                              const uint64_t* d_all_keys, int32_t* d_docs, float* d_scores,
-                              void* stream) {
+// The finish half on up to three streams: theta on st_theta, the REST pass
+// on st_rest (after theta: an event), the merges on st_sel (after REST).  One
+// stream for all three is bm25_search_finish_device.
+static int finish_impl(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, int32_t k,
+                       int32_t world, int64_t shard_docs_max, const uint64_t* d_all_keys,
+                       int32_t* d_docs, float* d_scores, hipStream_t st, hipStream_t st_rest,
+                       hipStream_t st_sel) {
   if (!h) return fail(BM25_EINVAL, "NULL index");
   if (Q < 0 || T < 0 || world < 1) return fail(BM25_EINVAL, "bad shape");
   int rc = check_k(h, k, true);
@@ -839,10 +845,21 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
   if (Q == 0 || k == 0) return BM25_OK;
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
-  const hipStream_t st = (hipStream_t)stream;
+  for (hipEvent_t& e : h->ev_split)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  // st_sel continues after everything enqueued on st (an event; none if equal)
+  auto join = [&](hipStream_t from, hipStream_t to, hipEvent_t e) -> hipError_t {
+    if (from == to) return hipSuccess;
+    hipError_t x = hipEventRecord(e, from);
+    return x != hipSuccess ? x : hipStreamWaitEvent(to, e, 0);
+  };
   if (k > kMaxK) {  // this shard's exact top-k (padded past its documents)
     h->sampled = false;
-    return run_search(h, d_queries, Q, T, k, d_docs, d_scores, st);
+    rc = run_search(h, d_queries, Q, T, k, d_docs, d_scores, st);
+    if (rc) return rc;
+    HIP_TRY(join(st, st_sel, h->ev_split[1]), "stream join");
+    if (st_sel != st) HIP_TRY(hipEventRecord(h->ws_done, st_sel), "hipEventRecord");
+    return BM25_OK;
   }
   rc = ensure_ws(h, Q, T, k, st);
   if (rc) return rc;
@@ -859,20 +876,47 @@ int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q
     h->ws.seq = h->seq;
   }
   h->sampled = false;
-  HIP_TRY(launch_finish(h->ix, d_queries, Q, T, k, g, world, d_all_keys, h->ws, st),
-          "finish launch");
   EventPair* ev = h->split_ev;
   h->split_ev = nullptr;
-  if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
-  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, g.P, h->ws, d_docs, d_scores, st),
+  // on three streams the score pass is timed on its own stream, from the
+  // REST pass's start (the sample half and theta ran on another stream)
+  HIP_TRY(launch_finish(h->ix, d_queries, Q, T, k, g, world, d_all_keys, h->ws, st, st_rest,
+                        h->ev_split[0], (ev && st_rest != st) ? ev->a : nullptr),
+          "finish launch");
+  if (ev) HIP_TRY(hipEventRecord(ev->b, st_rest), "hipEventRecord");
+  HIP_TRY(join(st_rest, st_sel, h->ev_split[1]), "stream join");
+  // world > 1: this shard's list goes to the W-way merge, which sorts (no
+  // sorted list needed here); world = 1 is a plain search: sorted
+  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, g.P, h->ws, d_docs, d_scores, st_sel,
+                        world > 1),
           "select launch");
-  if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
-  HIP_TRY(hipEventRecord(h->ws_done, st), "hipEventRecord");
+  if (ev) HIP_TRY(hipEventRecord(ev->c, st_sel), "hipEventRecord");
+  HIP_TRY(hipEventRecord(h->ws_done, st_sel), "hipEventRecord");
+  h->ws_stream = st_sel;  // (the next search on another stream waits for ws_done)
   if (h->prof) {
     h->score_launches += 1;
     h->searches += 1;
   }
   return BM25_OK;
+}
+
+int bm25_search_finish_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T,
+                              int32_t k, int32_t world, int64_t shard_docs_max,
+                              const uint64_t* d_all_keys, int32_t* d_docs, float* d_scores,
+                              void* stream) {
+  const hipStream_t st = (hipStream_t)stream;
+  return finish_impl(h, d_queries, Q, T, k, world, shard_docs_max, d_all_keys, d_docs, d_scores,
+                     st, st, st);
+}
+
+int bm25_search_finish_streams_device(bm25_index* h, const int32_t* d_queries, int64_t Q,
+                                      int64_t T, int32_t k, int32_t world,
+                                      int64_t shard_docs_max, const uint64_t* d_all_keys,
+                                      int32_t* d_docs, float* d_scores, void* stream_theta,
+                                      void* stream_rest, void* stream_select) {
+  return finish_impl(h, d_queries, Q, T, k, world, shard_docs_max, d_all_keys, d_docs, d_scores,
+                     (hipStream_t)stream_theta, (hipStream_t)stream_rest,
+                     (hipStream_t)stream_select);
 }
 
 int bm25_build_scores(int device, int64_t n_docs, int64_t n_terms, int64_t n_triples,

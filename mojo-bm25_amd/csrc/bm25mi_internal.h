@@ -247,14 +247,21 @@ hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
 hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                          const SampleGeom& g, uint64_t* keys, const Workspace& ws,
                          hipStream_t stream);
+// rest_stream (when not null and not `stream`): the REST pass runs there,
+// after theta (join: recorded on `stream`, waited on rest_stream); rest_timing
+// (optional) is recorded on rest_stream just before the REST pass.
 hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                          int k, const SampleGeom& g, int W, const uint64_t* all_keys,
-                         const Workspace& ws, hipStream_t stream);
+                         const Workspace& ws, hipStream_t stream,
+                         hipStream_t rest_stream = nullptr, hipEvent_t join = nullptr,
+                         hipEvent_t rest_timing = nullptr);
 // Merge (+ rescore + final merge), then the exact fallback stage; P = the
-// search's sampling stride.
+// search's sampling stride.  unsorted: a doc shard's list for the W-way merge
+// (the keys >= its k-th key in no order, padding last: merge_fast skips the
+// sort; the fallback stages still write sorted lists).
 hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries,
                          int64_t Q, int64_t T, int k, int P, const Workspace& ws,
-                         int32_t* d_docs, float* d_scores, hipStream_t stream);
+                         int32_t* d_docs, float* d_scores, hipStream_t stream, bool unsorted = false);
 hipError_t launch_scores_dense(const DevIndex& ix, const int32_t* d_query,
                                int64_t T, float* d_out, hipStream_t stream);
 // W lists [Q, k] at element w * rank_stride (docs and scores alike) -> [Q, k];

@@ -126,6 +126,8 @@ struct Stage {
                              // (zero at launch: each flat launch leaves its region zeroed)
   bool remap;                // merges: qmap gives the batch row of every array (the
                              // main stage's queries left to the block merge)
+  bool unsorted;             // merge_fast: a doc shard's list for the W-way merge — its
+                             // keys >= the k-th, in no order (padding last): no sort
 };
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -2426,6 +2428,123 @@ __global__ __launch_bounds__(kMergeNT) void merge_first_kernel(
 // merge_first_kernel (ws.slow).  Replaces the block-per-query sort of the
 // whole list (merge_first: 1024 threads, ~55 barrier-separated bitonic stages
 // over the padded list) for the common case.
+// ---- register bitonic sort of a wave's keys (R per lane, element j * 64 +
+// lane), best (largest) first.  Partners in other lanes come over DPP
+// (xor 1, 2: quad permutes), ds_swizzle (xor 4 .. 16, within 32 lanes) or
+// ds_bpermute (xor 32): no LDS memory round trips and no fences, where the
+// LDS bitonic of wave_sort_write waits on two LDS reads per step.
+template <int X>
+__device__ __forceinline__ uint32_t lane_xor32(uint32_t v) {
+  if constexpr (X == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (X == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (X < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (X << 10));
+  else return (uint32_t)__shfl_xor((int)v, X, 64);
+}
+template <int X>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
+  return ((uint64_t)lane_xor32<X>((uint32_t)(v >> 32)) << 32) | lane_xor32<X>((uint32_t)v);
+}
+// One compare-exchange step (block size SZ, partner distance ST) of the
+// bitonic network over 64 R elements, sorting descending.
+template <int R, int SZ, int ST>
+__device__ __forceinline__ void bitonic_step(uint64_t (&k)[R], uint32_t lane) {
+  if constexpr (ST >= 64) {
+    constexpr int js = ST / 64;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if ((j & js) == 0) {
+        const bool desc = ((j * 64) & SZ) == 0;  // (SZ >= 128: uniform per register)
+        const uint64_t a = k[j], b = k[j | js];
+        const bool sw = desc ? (a < b) : (a > b);
+        k[j] = sw ? b : a;
+        k[j | js] = sw ? a : b;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint64_t p = lane_xor64<ST>(k[j]);
+      const bool desc = (((uint32_t)j * 64u + lane) & (uint32_t)SZ) == 0u;
+      const bool low = (lane & (uint32_t)ST) == 0u;
+      const bool mx = low == desc;
+      k[j] = mx ? (k[j] > p ? k[j] : p) : (k[j] < p ? k[j] : p);
+    }
+  }
+}
+template <int R, int SZ, int ST>
+__device__ __forceinline__ void bitonic_merge(uint64_t (&k)[R], uint32_t lane) {
+  bitonic_step<R, SZ, ST>(k, lane);
+  if constexpr (ST > 1) bitonic_merge<R, SZ, ST / 2>(k, lane);
+}
+template <int R, int SZ>
+__device__ __forceinline__ void bitonic_sizes(uint64_t (&k)[R], uint32_t lane) {
+  bitonic_merge<R, SZ, SZ / 2>(k, lane);
+  if constexpr (SZ < 64 * R) bitonic_sizes<R, SZ * 2>(k, lane);
+}
+template <int R>
+__device__ __forceinline__ void wave_sort_regs(uint64_t (&k)[R]) {
+  bitonic_sizes<R, 2>(k, (uint32_t)lane_id());
+}
+
+// keys[0, n) of a wave's LDS slice (n <= 64 R), sorted best first in
+// registers; the first k written as docs / scores of row q (past n: doc -1,
+// score bits ~0).  Every key is read before any output is written.
+template <int R>
+__device__ __forceinline__ void regs_sort_write(const uint64_t* keys, uint32_t n, int32_t k,
+                                                int64_t doc_offset, int64_t q,
+                                                int32_t* __restrict__ docs,
+                                                float* __restrict__ scores) {
+  const uint32_t lane = lane_id();
+  uint64_t key[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const uint32_t i = (uint32_t)j * 64u + lane;
+    key[j] = i < n ? keys[i] : 0ull;
+  }
+  wave_sort_regs<R>(key);
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int i = j * 64 + (int)lane;
+    if (i < k) {
+      const uint64_t x = key[j];
+      if (x == 0ull) {  // padding (a shard holding fewer than k keys)
+        docs[q * k + i] = -1;
+        scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
+      } else {
+        docs[q * k + i] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)x) + doc_offset);
+        scores[q * k + i] = key_score((uint32_t)(x >> 32));
+      }
+    }
+  }
+  // k > 64 R (n <= 64 R): the rest is padding
+  for (int i = 64 * R + (int)lane; i < k; i += 64) {
+    docs[q * k + i] = -1;
+    scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
+  }
+}
+
+// n keys in the wave's LDS slice -> sorted and written: registers for n <=
+// 64 MAXR, the LDS bitonic above that.
+__device__ __forceinline__ void wave_sort_write(uint64_t* keys, uint32_t n, int m, int32_t k,
+                                                int64_t doc_offset, int64_t q,
+                                                int32_t* __restrict__ docs,
+                                                float* __restrict__ scores);
+template <int MAXR = 4>
+__device__ __forceinline__ void sort_write_any(uint64_t* keys, uint32_t n, int32_t k,
+                                               int64_t doc_offset, int64_t q,
+                                               int32_t* __restrict__ docs,
+                                               float* __restrict__ scores) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (n <= 128u)
+    regs_sort_write<2>(keys, n, k, doc_offset, q, docs, scores);
+  else if (MAXR >= 4 && n <= 256u)
+    regs_sort_write<4>(keys, n, k, doc_offset, q, docs, scores);
+  else if (MAXR >= 8 && n <= 512u)
+    regs_sort_write<MAXR >= 8 ? 8 : 2>(keys, n, k, doc_offset, q, docs, scores);
+  else
+    wave_sort_write(keys, n, next_pow2((int64_t)n), k, doc_offset, q, docs, scores);
+}
+
 constexpr int kFastR = 32;      // list keys per lane held in registers
 constexpr int kFastMaxK = 1024; // largest k served (LDS: k keys per wave)
 
@@ -2453,9 +2572,49 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
     key[j] = x >= th ? x : 0ull;  // (every list key is >= theta; key 0 = empty)
   }
   uint32_t n = 0;
+  if (!sg.unsorted && R <= 4) {
+    // a list of <= 256 keys: sorted whole in registers, its first k written
+    // (no selection)
+    wave_sort_regs<R>(key);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int i = j * 64 + (int)lane;
+      if (i < k) {
+        const uint64_t x = key[j];
+        docs[q * k + i] = x == 0ull ? -1 : (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)x) + doc_offset);
+        scores[q * k + i] = x == 0ull ? __uint_as_float(0xFFFFFFFFu) : key_score((uint32_t)(x >> 32));
+      }
+    }
+    for (int i = 64 * R + (int)lane; i < k; i += 64) {
+      docs[q * k + i] = -1;
+      scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
+    }
+    return;
+  }
   const uint64_t kth = wave_kth_key<R>(key, k, n);
+  if (sg.unsorted) {
+    // a doc shard's list for the W-way merge: the n kept keys in list order
+    // straight to the output, padding after them
+    uint32_t base = 0u;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const bool keep = key[j] != 0ull && key[j] >= kth;
+      const uint64_t b = __ballot(keep);
+      if (keep) {
+        const uint32_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        docs[q * k + i] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)key[j]) + doc_offset);
+        scores[q * k + i] = key_score((uint32_t)(key[j] >> 32));
+      }
+      base += (uint32_t)__popcll(b);
+    }
+    for (int i = (int)base + (int)lane; i < k; i += 64) {
+      docs[q * k + i] = -1;
+      scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
+    }
+    return;
+  }
   // the n kept keys (>= kth; unique: doc ids differ) -> LDS, sorted best first
-  const int m = next_pow2(n > 1u ? n : 2u);
   uint32_t base = 0u;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
@@ -2466,7 +2625,7 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
                                             __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
     base += (uint32_t)__popcll(b);
   }
-  wave_sort_write(keys, n, m, k, doc_offset, q, docs, scores);
+  sort_write_any(keys, n, k, doc_offset, q, docs, scores);
 }
 
 // The k-th largest of a wave's keys held R per lane (key 0 = empty; keys
@@ -2901,6 +3060,8 @@ __device__ __forceinline__ void lds_merge_one(uint64_t* kb, uint32_t cnt, int32_
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
     base += (uint32_t)__popcll(b);
   }
+  // (the LDS bitonic: the register sort here would make merge_fast_kernel,
+  // which inlines this for long lists, spill)
   wave_sort_write(kb, kept, next_pow2(kept > 1u ? kept : 2u), k, doc_offset, q, docs, scores);
 }
 
@@ -2914,44 +3075,43 @@ __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
   if (q >= Q) return;  // wave-uniform; no barriers
   uint64_t* kb = buf[wave];
   const uint32_t lane = lane_id();
-  const int n = W * k;
-  constexpr int U = kMergeSortedCap / 64;
-  float sv[U];
-  int32_t dv[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = u * 64 + (int)lane;
-    const int w = i / k, j = i - w * k;
-    const int64_t o = (int64_t)w * rstride + q * k + j;
-    sv[u] = i < n ? in_scores[o] : 0.f;
-    dv[u] = i < n ? in_docs[o] : -1;
-  }
-  uint64_t key[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = u * 64 + (int)lane;
-    key[u] = i < n ? make_key(sv[u], (uint32_t)dv[u]) : 0ull;  // (padding: key 0)
-  }
   // the lists' real keys (most slots are padding: the world holds ~2-3 k keys
-  // >= theta) compacted into LDS, then selected from the fewest registers
+  // >= theta) compacted into the wave's LDS slice: rank by rank, columns of
+  // 64 (all loads of a rank in flight; no index division)
   uint32_t cnt = 0u;
+  const int nc = (k + 63) >> 6;
+  for (int w = 0; w < W; ++w) {
+    const int64_t o = (int64_t)w * rstride + q * k;
+    for (int c0 = 0; c0 < nc; c0 += 4) {
+      float sv[4];
+      int32_t dv[4];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const bool nz = key[u] != 0ull;
-    const uint64_t b = __ballot(nz);
-    if (nz)
-      kb[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                         __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[u];
-    cnt += (uint32_t)__popcll(b);
+      for (int u = 0; u < 4; ++u) {
+        const int j = (c0 + u) * 64 + (int)lane;
+        const bool in = c0 + u < nc && j < k;
+        sv[u] = in ? in_scores[o + j] : 0.f;
+        dv[u] = in ? in_docs[o + j] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool nz = dv[u] >= 0;  // (padding: doc -1)
+        const uint64_t b = __ballot(nz);
+        if (nz)
+          kb[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
+              make_key(sv[u], (uint32_t)dv[u]);
+        cnt += (uint32_t)__popcll(b);
+      }
+    }
+  }
+  // <= 512 keys: sorted whole in registers, the first k written; more: the
+  // k-th key selected first, the keys at or above it sorted
+  if (cnt <= 512u) {
+    sort_write_any<8>(kb, cnt, k, 0, q, docs, scores);
+    return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  const uint32_t nj = (cnt + 63u) >> 6;
-  if (nj <= 4u)
-    lds_merge_one<4>(kb, cnt, k, 0, q, docs, scores);
-  else if (nj <= 8u)
-    lds_merge_one<8>(kb, cnt, k, 0, q, docs, scores);
-  else
-    lds_merge_one<U>(kb, cnt, k, 0, q, docs, scores);
+  lds_merge_one<kMergeSortedCap / 64>(kb, cnt, k, 0, q, docs, scores);
 }
 
 // ---------------------------------------------------------------------------
@@ -3306,13 +3466,25 @@ static void sample_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
 template <int S_>
 static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
                      const SampleGeom& g, int W, const uint64_t* all_keys, const Workspace& ws,
-                     hipStream_t st, bool theta_ready = false) {
+                     hipStream_t st, bool theta_ready = false, hipStream_t st_rest = nullptr,
+                     hipEvent_t join = nullptr, hipEvent_t rest_timing = nullptr) {
   Stage sg = main_stage(ix, Q, g.P, ws);
+  // the score pass's stream: after everything enqueued on st so far
+  auto to_rest = [&]() -> hipStream_t {
+    if (st_rest == nullptr || st_rest == st || join == nullptr) {
+      if (rest_timing) hipEventRecord(rest_timing, st);
+      return st;
+    }
+    hipEventRecord(join, st);
+    hipStreamWaitEvent(st_rest, join, 0);
+    if (rest_timing) hipEventRecord(rest_timing, st_rest);
+    return st_rest;
+  };
   if (g.P == 1) {  // no sample pass ran: nothing was zeroed, no segment table built
     hipMemsetAsync(ws.counters, 0, kCounters * sizeof(int32_t), st);
     if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, q, Q, T, ws, st);
     sg.ctr_region = 2;
-    launch_phase<S_, kAll>(ix, q, T, Q, sg, ws, st);
+    launch_phase<S_, kAll>(ix, q, T, Q, sg, ws, to_rest());
     return;
   }
   sg.ctr_region = 1;  // counters and list counts: reset by theta_wave_kernel
@@ -3326,7 +3498,7 @@ static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
     hipLaunchKernelGGL(theta_wave_kernel, dim3((unsigned)((Q + kQW - 1) / kQW)), dim3(64 * kQW), 0, st,
                        all_keys, (int64_t)W, Q, g.S, (int32_t)k, ws.theta, ws.list_cnt,
                        ws.list_cap, ix.nonneg ? 1 : 0, ix.doc_offset, ix.n_docs, ws.counters);
-  launch_phase<S_, kRest>(ix, q, T, Q, sg, ws, st);
+  launch_phase<S_, kRest>(ix, q, T, Q, sg, ws, to_rest());
 }
 
 #define BM25_SHIFT_DISPATCH(call)                        \
@@ -3362,9 +3534,18 @@ hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q
 
 hipError_t launch_finish(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                          int k, const SampleGeom& g, int W, const uint64_t* all_keys,
-                         const Workspace& ws, hipStream_t stream) {
-  if (Q == 0 || ix.ntiles == 0) return hipSuccess;
-#define CALL(s) finish_s<s>(ix, d_queries, Q, T, k, g, W, all_keys, ws, stream)
+                         const Workspace& ws, hipStream_t stream, hipStream_t rest_stream,
+                         hipEvent_t join, hipEvent_t rest_timing) {
+  if (Q == 0 || ix.ntiles == 0) {
+    if (rest_stream && rest_stream != stream && join) {  // (the caller's order still holds)
+      hipEventRecord(join, stream);
+      hipStreamWaitEvent(rest_stream, join, 0);
+    }
+    if (rest_timing) hipEventRecord(rest_timing, rest_stream ? rest_stream : stream);
+    return hipGetLastError();
+  }
+#define CALL(s) finish_s<s>(ix, d_queries, Q, T, k, g, W, all_keys, ws, stream, false, \
+                            rest_stream, join, rest_timing)
   BM25_SHIFT_DISPATCH(CALL)
 #undef CALL
   return hipGetLastError();
@@ -3464,8 +3645,10 @@ static void select_stage(const DevIndex& ix, const int32_t* q, int64_t T, int k,
 
 template <int S_>
 static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k, int P,
-                     const Workspace& ws, int32_t* docs, float* scores, hipStream_t st) {
-  const Stage ms = main_stage(ix, Q, P, ws);
+                     const Workspace& ws, int32_t* docs, float* scores, hipStream_t st,
+                     bool unsorted) {
+  Stage ms = main_stage(ix, Q, P, ws);
+  ms.unsorted = unsorted;
   select_stage<S_>(ix, q, T, k, ms, ws, docs, scores, st);
   if (P == 1) return;
   // queries whose list overflowed: exact pass over every tile (usually none;
@@ -3490,14 +3673,14 @@ static void select_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T,
 
 hipError_t launch_select(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
                          int k, int P, const Workspace& ws, int32_t* d_docs, float* d_scores,
-                         hipStream_t stream) {
+                         hipStream_t stream, bool unsorted) {
   if (Q == 0 || k == 0) return hipSuccess;
   if (ix.ntiles == 0) {  // an empty doc shard: an all-padding list (doc -1, score bits ~0)
     hipMemsetAsync(d_docs, 0xFF, sizeof(int32_t) * Q * k, stream);
     hipMemsetAsync(d_scores, 0xFF, sizeof(float) * Q * k, stream);
     return hipGetLastError();
   }
-#define CALL(s) select_s<s>(ix, d_queries, Q, T, k, P, ws, d_docs, d_scores, stream)
+#define CALL(s) select_s<s>(ix, d_queries, Q, T, k, P, ws, d_docs, d_scores, stream, unsorted)
   BM25_SHIFT_DISPATCH(CALL)
 #undef CALL
   return hipGetLastError();

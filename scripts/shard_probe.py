@@ -152,6 +152,116 @@ def rank_pipelined(shards, forks, r, q, k, W, smax, keys_c, g_c, outs, streams, 
                         2 * q.shape[0] * k, outs[i][0], outs[i][1], st)
 
 
+def run_gated(shards, forks, r, q, k, W, smax, keys_c, g_c, outs, streams, comm, keys_us,
+              list_us, nb):
+    """`nb` consecutive batches of rank r, software-pipelined over two
+    contexts (the shard's handle and a fork, own streams, keys, lists and
+    outputs): batch b+1's threshold half (bound keys + key all-gather) is
+    issued before batch b's list all-gather and starts once batch b's finish
+    half has started (an event), so it runs beside batch b's REST pass and
+    fills its tail instead of following its merges; the REST passes stay in
+    batch order.  Collectives: modelled spin kernels on the one comm stream,
+    issued in the same order on every rank."""
+    ctx = [shards[r]] + forks
+    dev = q.device.index
+
+    def coll(st, us):
+        if us <= 0:
+            return
+        e = torch.cuda.Event()
+        e.record(st)
+        comm.wait_event(e)
+        sleep_us(us, comm)
+        e2 = torch.cuda.Event()
+        e2.record(comm)
+        st.wait_event(e2)
+
+    main_st = torch.cuda.current_stream()
+    e0 = torch.cuda.Event()
+    e0.record(main_st)
+    for s_ in streams:
+        s_.wait_event(e0)
+    ctx[0].search_sample_device(q, k, W, smax, keys_c[0][r], streams[0])
+    coll(streams[0], keys_us)
+    for b in range(nb):
+        i, j = b % 2, (b + 1) % 2
+        st = streams[i]
+        gate = torch.cuda.Event()
+        gate.record(st)
+        ctx[i].search_finish_device(q, k, W, smax, keys_c[i], g_c[i][r, 0],
+                                    g_c[i][r, 1].view(torch.float32), st)
+        if b + 1 < nb:
+            streams[j].wait_event(gate)
+            ctx[j].search_sample_device(q, k, W, smax, keys_c[j][r], streams[j])
+            coll(streams[j], keys_us)
+        coll(st, list_us)
+        if W > 1:
+            merge_sorted_device(dev, g_c[i], g_c[i][:, 1].view(torch.float32), W, q.shape[0], k,
+                                2 * q.shape[0] * k, outs[i][0], outs[i][1], st)
+    for s_ in streams:
+        e = torch.cuda.Event()
+        e.record(s_)
+        main_st.wait_event(e)
+
+
+def run_streams(ctxs, r, q, k, W, smax, keys_c, g_c, outs, sp, comm, keys_us, list_us, nb,
+                post_ev):
+    """`nb` consecutive batches of rank r on three streams (sp = pre, rest,
+    post) and C = len(ctxs) contexts: batch b's threshold (sample half, key
+    all-gather, theta) on `pre`, its REST pass on `rest` (batch order), its
+    merges, list all-gather and W-way merge on `post`
+    (bm25_search_finish_streams_device).  Batch b+1's sample half starts
+    once the batch that last used its context (b+1-C) has merged.
+    Collectives: modelled spin kernels on the comm stream, issued in one
+    order on every rank (keys of b+1 before the lists of b)."""
+    C = len(ctxs)
+    pre, rest, post = sp
+    dev = q.device.index
+
+    def coll(st, us):
+        if us <= 0:
+            return
+        e = torch.cuda.Event()
+        e.record(st)
+        comm.wait_event(e)
+        sleep_us(us, comm)
+        e2 = torch.cuda.Event()
+        e2.record(comm)
+        st.wait_event(e2)
+
+    main_st = torch.cuda.current_stream()
+    e0 = torch.cuda.Event()
+    e0.record(main_st)
+    for s_ in sp:
+        s_.wait_event(e0)
+
+    def sample(b):
+        i = b % C
+        if post_ev[i] is not None:
+            pre.wait_event(post_ev[i])
+        ctxs[i].search_sample_device(q, k, W, smax, keys_c[i][r], pre)
+        coll(pre, keys_us)
+
+    sample(0)
+    for b in range(nb):
+        i = b % C
+        ctxs[i].search_finish_streams_device(q, k, W, smax, keys_c[i], g_c[i][r, 0],
+                                             g_c[i][r, 1].view(torch.float32), pre, rest, post)
+        if b + 1 < nb:
+            sample(b + 1)
+        coll(post, list_us)
+        if W > 1:
+            merge_sorted_device(dev, g_c[i], g_c[i][:, 1].view(torch.float32), W, q.shape[0], k,
+                                2 * q.shape[0] * k, outs[i][0], outs[i][1], post)
+        e = torch.cuda.Event()
+        e.record(post)
+        post_ev[i] = e
+    for s_ in sp:
+        e = torch.cuda.Event()
+        e.record(s_)
+        main_st.wait_event(e)
+
+
 def main():
     cfg = synth.CONFIGS["c3"]
     nq = int(os.environ.get("PROBE_Q", "0")) or None  # batch size (default: the config's 1024)
@@ -164,6 +274,9 @@ def main():
     grids = [int(x) for x in os.environ.get("PROBE_GRID", "100").split(",")]
     hybrid = os.environ.get("PROBE_HYBRID") == "1"
     pipe = int(os.environ.get("PROBE_PIPE", "1"))  # batches in flight per rank
+    gated = os.environ.get("PROBE_GATED") == "1"   # run_gated: two batches, threshold ahead
+    nctx = int(os.environ.get("PROBE_STREAMS", "0"))  # run_streams with this many contexts
+    gated = gated or nctx > 0
     w1_ms = None
     jobs = [(int(x), 1) for x in (sys.argv[1:] or ["1", "2", "4", "8"])]
     if hybrid:  # 2 replicas x W/2 shards: each rank half the batch on a 2/W shard
@@ -191,7 +304,8 @@ def main():
                 cuts = [Q * i // P for i in range(P + 1)]
                 rows = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
                 inline = P > 1 or os.environ.get("PROBE_INLINE") == "1"
-                if W == 1 and P == 1 and pipe > 1:  # batches in flight on forks, own streams
+                many = None
+                if W == 1 and P == 1 and pipe > 1 and not gated:  # batches in flight on forks, own streams
                     wforks = [shards[0]] + [shards[0].fork() for _ in range(pipe - 1)]
                     wstreams = [torch.cuda.Stream() for _ in range(pipe)]
                     wouts = [(torch.empty_like(out_d), torch.empty_like(out_s))
@@ -202,7 +316,7 @@ def main():
                         i = wstep[0] % pipe
                         wforks[i].search_device(q, k, wouts[i][0], wouts[i][1], wstreams[i])
                         wstep[0] += 1
-                elif W == 1 and P == 1:
+                elif W == 1 and P == 1 and not gated:
                     def one(r):
                         shards[0].search_device(q, k, out_d, out_s, st)
                 else:
@@ -220,7 +334,40 @@ def main():
                         keys_p.append(kk)
                         g_p.append(g)
                     torch.cuda.synchronize()
-                    if pipe > 1:
+                    if nctx > 0:
+                        sforks = {}
+                        sstreams = [torch.cuda.Stream() for _ in range(3)]
+                        scomm = torch.cuda.Stream()
+                        kus = model_gather_us(keys_b, W)
+                        lus = model_gather_us(list_b, W)
+                        keys_c = [keys_p[0]] + [keys_p[0].clone() for _ in range(nctx - 1)]
+                        g_c = [g_p[0]] + [g_p[0].clone() for _ in range(nctx - 1)]
+                        outs = [(torch.empty_like(out_d), torch.empty_like(out_s))
+                                for _ in range(nctx)]
+
+                        def many(r, nb):
+                            if r not in sforks:
+                                sforks[r] = ([shards[r]] + [shards[r].fork()
+                                                            for _ in range(nctx - 1)],
+                                             [None] * nctx)
+                            run_streams(sforks[r][0], r, q, k, W, smax, keys_c, g_c, outs,
+                                        sstreams, scomm, kus, lus, nb, sforks[r][1])
+                    elif gated:
+                        gforks = {}
+                        gstreams = [torch.cuda.Stream() for _ in range(2)]
+                        gcomm = torch.cuda.Stream()
+                        kus = model_gather_us(keys_b, W)
+                        lus = model_gather_us(list_b, W)
+                        keys_c = [keys_p[0], keys_p[0].clone()]
+                        g_c = [g_p[0], g_p[0].clone()]
+                        outs = [(torch.empty_like(out_d), torch.empty_like(out_s)) for _ in range(2)]
+
+                        def many(r, nb):
+                            if r not in gforks:
+                                gforks[r] = [shards[r].fork()]
+                            run_gated(shards, gforks[r], r, q, k, W, smax, keys_c, g_c, outs,
+                                      gstreams, gcomm, kus, lus, nb)
+                    elif pipe > 1:
                         pforks = {}
                         pstreams = [torch.cuda.Stream() for _ in range(pipe)]
                         pcomm = torch.cuda.Stream()
@@ -278,6 +425,16 @@ def main():
                          [int(x) for x in ranks_env.split(",") if int(x) < W])
                 per_rank = []
                 for r in ranks:
+                    if many is not None:  # the pipelined batches: n in one issue sequence
+                        many(r, 3)
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        many(r, n)
+                        torch.cuda.synchronize()
+                        ms = (time.perf_counter() - t0) * 1e3 / n
+                        per_rank.append({"rank": r, "ms": round(ms, 4), "fallback_queries":
+                                         shards[r].search_stats()["fallback_queries"]})
+                        continue
                     for _ in range(3):
                         one(r)
                     torch.cuda.synchronize()
@@ -289,7 +446,7 @@ def main():
                     per_rank.append({"rank": r, "ms": round(ms, 4),
                                      "fallback_queries": shards[r].search_stats()["fallback_queries"]})
                 worst = max(x["ms"] for x in per_rank)
-                inline = inline or pipe > 1
+                inline = inline or pipe > 1 or gated
                 coll_us = 0.0 if inline else (model_gather_us(list_b, W) if
                                               os.environ.get("PROBE_LOCAL") == "1" else
                                               model_gather_us(keys_b, W) + model_gather_us(list_b, W))
@@ -297,7 +454,9 @@ def main():
                 if W == 1 and P == 1 and R == 1 and gp == 100:
                     w1_ms = worst
                 line = {"W": W * R, "shards": W, "replicas": R, "parts": P, "grid_pct": gp,
-                        "batches_in_flight": pipe if W > 1 else 1,
+                        "batches_in_flight": 2 if gated else (pipe if W > 1 else 1),
+                        "pipeline": (f"three streams, {nctx} contexts (run_streams)" if nctx
+                                     else "gated (run_gated)" if gated else None),
                         "queries_per_rank": Q, "shard_docs_max": smax, "sample_width": S,
                         "per_rank": per_rank, "max_rank_ms": round(worst, 4),
                         "model": {"alpha_us": ALPHA_US, "link_GBps": LINK_GBS,
