@@ -321,7 +321,10 @@ int bm25_sharded_destroy(bm25_sharded* s);
  * Timing of the score pass (sample + theta + rest score kernels, the HBM
  * bound part of a search), measured with HIP events recorded on the search
  * stream around it in every search while enabled.
- * bm25_profile_enable(idx, 1) resets the accumulators.
+ * bm25_profile_enable(idx, on) resets the accumulators; on = 1: two events
+ * per search (score pass start and end: total_ms reports the score pass);
+ * on = 2: a third at the search's end (total_ms = the whole search).  Each
+ * event record costs the device a marker packet (~4 us).
  */
 int bm25_profile_enable(bm25_index* idx, int on);
 int bm25_profile_read(bm25_index* idx, double* score_ms_total,

@@ -234,7 +234,7 @@ class GpuIndex:
 
     # ------------------------------------------------------------------
     def profile_enable(self, on: bool = True) -> None:
-        check(lib.bm25_profile_enable(self._h, int(on)))
+        check(lib.bm25_profile_enable(self._h, int(on)))  # (True = 1: score pass events only)
 
     def profile_read(self) -> dict:
         sm = ctypes.c_double()

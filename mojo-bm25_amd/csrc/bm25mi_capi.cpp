@@ -53,6 +53,7 @@ int env_int(const char* name, int dflt) {
 
 struct EventPair {
   hipEvent_t a = nullptr, b = nullptr, c = nullptr;  // start, after score pass, end
+  bool with_c = false;                                 // c recorded (profiling level 2)
 };
 
 // The device arrays of one built index, shared by the handle that built it
@@ -80,16 +81,16 @@ struct bm25_index {
   int64_t cap_q_elems = 0, cap_out_elems = 0;
   std::mutex mu;
   // profiling
-  bool prof = false;
+  int prof = 0;  // 1: score pass events (a, b) per search; 2: also the search's end (c)
   std::vector<EventPair> ev_pool;
   size_t ev_used = 0;
   double score_ms = 0.0, total_ms = 0.0;
   int64_t score_launches = 0, searches = 0, rescored = 0;
   int64_t device_bytes = 0;
   EventPair* split_ev = nullptr;  // events of a sample/finish search in flight
-  hipEvent_t ws_done = nullptr;    // end of the last search that used the workspace
+  hipEvent_t ws_done = nullptr;    // recorded on ws_stream when a search moves to another stream
   hipEvent_t ev_split[2] = {nullptr, nullptr};  // theta -> REST, REST -> select (three streams)
-  hipStream_t ws_stream = nullptr; // its stream
+  hipStream_t ws_stream = nullptr; // the stream of the last search that used the workspace
   int32_t* d_maxtok = nullptr;     // bm25_max_token_device result
   bool sampled = false;            // a sample half ran since the last finish half
   // the threshold source (choose_theta_source): host-mapped report of the
@@ -286,11 +287,12 @@ void harvest_events(bm25_index* h) {
   if (h->ev_used == 0) return;
   for (size_t i = 0; i < h->ev_used; ++i) {
     float ms1 = 0.f, ms2 = 0.f;
-    hipEventSynchronize(h->ev_pool[i].c);  // events may sit on a caller's stream
+    const bool tot = h->ev_pool[i].with_c;
+    hipEventSynchronize(tot ? h->ev_pool[i].c : h->ev_pool[i].b);  // (maybe a caller's stream)
     hipEventElapsedTime(&ms1, h->ev_pool[i].a, h->ev_pool[i].b);
-    hipEventElapsedTime(&ms2, h->ev_pool[i].a, h->ev_pool[i].c);
+    if (tot) hipEventElapsedTime(&ms2, h->ev_pool[i].a, h->ev_pool[i].c);
     h->score_ms += ms1;
-    h->total_ms += ms2;
+    h->total_ms += tot ? ms2 : ms1;
   }
   h->ev_used = 0;
 }
@@ -308,22 +310,42 @@ EventPair* next_events(bm25_index* h) {
       harvest_events(h);
     }
   }
-  return &h->ev_pool[h->ev_used++];
+  EventPair* e = &h->ev_pool[h->ev_used++];
+  e->with_c = h->prof >= 2;
+  return e;
+}
+
+// Records the search's end event of a profiled search (level 2 only: every
+// event record is a marker packet the device spends ~4 us on).
+hipError_t record_end(bm25_index* h, EventPair* ev, hipStream_t st) {
+  return (ev && ev->with_c) ? hipEventRecord(ev->c, st) : hipSuccess;
 }
 
 // The workspace is shared by every search on the handle: a search enqueued
-// on another stream than the previous one first waits for that search's end
-// (ws_done, recorded after every search).
+// on another stream than the previous one first waits for everything
+// enqueued on that stream so far (ws_done, recorded there now).  Searches
+// that stay on one stream record nothing: an event record costs the device
+// a marker packet (~4 us, measured: scripts/dev/latency_bench.hip), a
+// cross-stream wait more.  The previous search's stream must still exist
+// (torch's pooled streams do).
 hipError_t order_ws(bm25_index* h, hipStream_t st) {
-  if (!h->ws_done) {
-    const hipError_t e = hipEventCreateWithFlags(&h->ws_done, hipEventDisableTiming);
-    if (e != hipSuccess) return e;
+  if (h->ws_stream == nullptr || st == h->ws_stream) {
     h->ws_stream = st;
     return hipSuccess;
   }
-  if (st == h->ws_stream) return hipSuccess;
+  if (!h->ws_done) {
+    const hipError_t e = hipEventCreateWithFlags(&h->ws_done, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipEventRecord(h->ws_done, h->ws_stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(st, h->ws_done, 0);
   h->ws_stream = st;
-  return hipStreamWaitEvent(st, h->ws_done, 0);
+  return e;
+}
+
+// The host waits for the workspace's last search (its stream).
+void ws_wait_host(bm25_index* h) {
+  if (h->ws_stream) hipStreamSynchronize(h->ws_stream);
 }
 
 // The threshold source of the handle's next search (DevIndex::bound_weak).
@@ -397,7 +419,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
     // the scratch the large-k paths last asked for, allocated once for the
     // next ones (the device is done with the old arena: its last search is)
     if (h->arena.need > h->arena.bytes) {
-      if (h->ws_done) HIP_TRY(hipEventSynchronize(h->ws_done), "hipEventSynchronize");
+      if (h->ws_stream) HIP_TRY(hipStreamSynchronize(h->ws_stream), "hipStreamSynchronize");
       hipFree(h->arena.base);
       h->arena.base = nullptr;
       h->arena.bytes = 0;
@@ -427,9 +449,8 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
     }
     if (ev) {
       HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
-      HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
+      HIP_TRY(record_end(h, ev, st), "hipEventRecord");
     }
-    HIP_TRY(hipEventRecord(h->ws_done, st), "hipEventRecord");
     if (h->prof) {
       h->score_launches += 1;
       h->searches += 1;
@@ -451,8 +472,7 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
   HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, P, h->ws, d_docs, d_scores, st),
           "select launch");
-  if (ev) HIP_TRY(hipEventRecord(ev->c, st), "hipEventRecord");
-  HIP_TRY(hipEventRecord(h->ws_done, st), "hipEventRecord");
+  HIP_TRY(record_end(h, ev, st), "hipEventRecord");
   if (h->prof) {
     h->score_launches += 1;
     h->searches += 1;
@@ -461,10 +481,10 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
 }
 
 // Counters of the last search (caller holds h->mu); the search may run on a
-// caller's stream: wait for its end event (ws_done), not for the device.
+// caller's stream: wait for that stream, not for the device.
 void read_counters(bm25_index* h, int32_t (&cnt)[kCounters]) {
   if (!h->ws.counters) return;
-  if (h->ws_done) hipEventSynchronize(h->ws_done);
+  ws_wait_host(h);
   hipMemcpyAsync(cnt, h->ws.counters, sizeof cnt, hipMemcpyDeviceToHost, h->stream);
   hipStreamSynchronize(h->stream);
 }
@@ -651,7 +671,9 @@ int bm25_index_destroy(bm25_index* h) {
   if (!h) return BM25_OK;
   hipSetDevice(h->ix.device);
   if (h->stream) hipStreamSynchronize(h->stream);
-  if (h->ws_done) hipEventSynchronize(h->ws_done);  // a search on a caller's stream
+  // a search on a caller's stream (which the caller may have destroyed since:
+  // the device, not the stream)
+  if (h->ws_stream) hipDeviceSynchronize();
   for (auto& p : h->ev_pool) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
@@ -858,7 +880,7 @@ static int finish_impl(bm25_index* h, const int32_t* d_queries, int64_t Q, int64
     rc = run_search(h, d_queries, Q, T, k, d_docs, d_scores, st);
     if (rc) return rc;
     HIP_TRY(join(st, st_sel, h->ev_split[1]), "stream join");
-    if (st_sel != st) HIP_TRY(hipEventRecord(h->ws_done, st_sel), "hipEventRecord");
+    if (st_sel != st) h->ws_stream = st_sel;  // (after the join: st_sel waits for st)
     return BM25_OK;
   }
   rc = ensure_ws(h, Q, T, k, st);
@@ -890,9 +912,8 @@ static int finish_impl(bm25_index* h, const int32_t* d_queries, int64_t Q, int64
   HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, g.P, h->ws, d_docs, d_scores, st_sel,
                         world > 1),
           "select launch");
-  if (ev) HIP_TRY(hipEventRecord(ev->c, st_sel), "hipEventRecord");
-  HIP_TRY(hipEventRecord(h->ws_done, st_sel), "hipEventRecord");
-  h->ws_stream = st_sel;  // (the next search on another stream waits for ws_done)
+  HIP_TRY(record_end(h, ev, st_sel), "hipEventRecord");
+  h->ws_stream = st_sel;  // (the next search on another stream waits for this one)
   if (h->prof) {
     h->score_launches += 1;
     h->searches += 1;
@@ -1150,7 +1171,7 @@ int bm25_profile_enable(bm25_index* h, int on) {
   std::lock_guard<std::mutex> lk(h->mu);
   hipSetDevice(h->ix.device);
   harvest_events(h);
-  h->prof = on != 0;
+  h->prof = on < 0 ? 0 : (on > 2 ? 2 : on);
   h->score_ms = h->total_ms = 0.0;
   h->score_launches = h->searches = h->rescored = 0;
   return BM25_OK;
@@ -1214,7 +1235,7 @@ int bm25_index_set_option(bm25_index* h, const char* name, int64_t value) {
   if (rc) return rc;
   if (h->ix.opt.list_cap != old_cap && h->ws.cap_q > 0) {  // the list capacity is sized in
     hipSetDevice(h->ix.device);                            // the workspace: rebuild it
-    if (h->ws_done) hipEventSynchronize(h->ws_done);
+    ws_wait_host(h);
     free_ws(h->ws);
   }
   return BM25_OK;

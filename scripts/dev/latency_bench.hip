@@ -121,6 +121,38 @@ int main() {
   CK(hipMemset(d_list, 0x11, sizeof(uint64_t) * Q * C));
 
   time_it("empty (256 x 256)", [&] { hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, 0, d_o); });
+  {
+    hipEvent_t e1, e2, e3;
+    CK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&e2, hipEventDisableTiming | hipEventReleaseToDevice));
+    CK(hipEventCreate(&e3));
+    time_it("empty + record(disable timing)", [&] {
+      hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, 0, d_o);
+      hipEventRecord(e1, 0);
+    });
+    time_it("empty + record(disable timing, release to device)", [&] {
+      hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, 0, d_o);
+      hipEventRecord(e2, 0);
+    });
+    time_it("empty + record(default)", [&] {
+      hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, 0, d_o);
+      hipEventRecord(e3, 0);
+    });
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    time_it("empty + record + wait on 2nd stream + empty there", [&] {
+      hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, 0, d_o);
+      hipEventRecord(e1, 0);
+      hipStreamWaitEvent(s2, e1, 0);
+      hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, s2, d_o);
+      hipEventRecord(e2, s2);
+      hipStreamWaitEvent(0, e2, 0);
+    });
+    time_it("empty x2 same stream", [&] {
+      hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, 0, d_o);
+      hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, 0, d_o);
+    });
+  }
   time_it("load1 (256 x 256)", [&] { hipLaunchKernelGGL(k_load1, dim3(Q), dim3(256), 0, 0, d_i, d_o); });
   time_it("chain3 (256 x 256)", [&] { hipLaunchKernelGGL(k_chain3, dim3(Q), dim3(256), 0, 0, d_i, d_o, Q * 256); });
   time_it("copy_list (wave per query)", [&] {
