@@ -225,9 +225,9 @@ int bm25_merge_topk_device(int device, const int32_t* d_docs,
                            void* stream);
 
 /*
- * The same merge for lists that are each already best first — what
- * bm25_search_finish_device writes (padding, doc -1 / key 0, last) — in one
- * buffer per rank: rank w's [Q, k] docs and scores start at element
+ * The same merge for the lists bm25_search_finish_device (world > 1) and
+ * bm25_search_shard_device write — a shard's keys in any order, padding
+ * (doc -1) anywhere — in one buffer per rank: rank w's [Q, k] docs and scores start at element
  * w * rank_stride of d_docs / d_scores (rank_stride = Q * k for plain
  * [W, Q, k] arrays, 2 * Q * k for the packed [W][docs|scores][Q][k] buffer
  * one all-gather moves).  A W-way merge, one wavefront per query.
@@ -285,6 +285,33 @@ int bm25_search_finish_streams_device(bm25_index* idx, const int32_t* d_queries,
                                       int64_t shard_docs_max, const uint64_t* d_all_keys,
                                       int32_t* d_docs, float* d_scores, void* stream_theta,
                                       void* stream_rest, void* stream_select);
+
+/*
+ * Doc-sharded search with ONE collective (the multi-process form used by
+ * bm25mi.dist when the collection's tile bounds fit one selection block:
+ * <= 30720 tiles).  Every rank exports its tile bounds, the ranks all-gather
+ * them once (at index build), and each rank's search takes the whole
+ * collection's tile-bound threshold by itself:
+ *   bm25_index_bounds_export(idx, d_out, stride, stream): this index's tile
+ *     bounds [n_terms][stride] u16 (stride: a multiple of 4 >= its tiles,
+ *     rounded up to 4; the same on every rank; zero past its tiles);
+ *   (caller) all-gather -> d_world [world][n_terms][stride], kept alive;
+ *   bm25_index_set_world_bounds(idx, d_world, world, stride, world_tiles):
+ *     world_tiles = the collection's tiles (NULL d_world clears);
+ *   bm25_search_shard_device(...): this shard's keys >= the collection's
+ *     threshold (k real documents score at least it) as a [Q, k] list in no
+ *     particular order (global doc ids, padding doc -1 / score bits
+ *     0xFFFFFFFF last), or its exact top-k for k > 4096 / queries the
+ *     threshold cannot serve;
+ *   (caller) all-gather the lists, bm25_merge_sorted_device (any order in).
+ * The result is exactly the single-index top-k.  Replaces no reference call:
+ * the reference is single-device (main.py:205).
+ */
+int bm25_index_bounds_export(bm25_index* idx, uint16_t* d_out, int64_t stride, void* stream);
+int bm25_index_set_world_bounds(bm25_index* idx, const uint16_t* d_world, int32_t world,
+                                int64_t stride, int64_t world_tiles);
+int bm25_search_shard_device(bm25_index* idx, const int32_t* d_queries, int64_t Q, int64_t T,
+                             int32_t k, int32_t* d_docs, float* d_scores, void* stream);
 
 /*
  * Doc-sharded index over several devices of ONE process.

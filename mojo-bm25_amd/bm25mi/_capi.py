@@ -85,6 +85,9 @@ _SIGS = {
                                            _P, _P], ctypes.c_int),
     "bm25_search_finish_device": ([_P, _P, _I64, _I64, _I32, _I32, _I64, _P, _P, _P, _P],
                                   ctypes.c_int),
+    "bm25_index_bounds_export": ([_P, _P, _I64, _P], ctypes.c_int),
+    "bm25_index_set_world_bounds": ([_P, _P, _I32, _I64, _I64], ctypes.c_int),
+    "bm25_search_shard_device": ([_P, _P, _I64, _I64, _I32, _P, _P, _P], ctypes.c_int),
     "bm25_build_scores": ([ctypes.c_int, _I64, _I64, _I64, _P, _P, _P, _P, ctypes.c_double,
                            ctypes.c_double, ctypes.c_double, ctypes.c_int, _P, _P, _P, _P, _P],
                           ctypes.c_int),

@@ -118,6 +118,42 @@ def _agree_width(index, S: int, k: int, device, group=None) -> None:
     seen.add(key)
 
 
+BOUND_MAX_TILES = 30720  # tiles one block selects a threshold over (kBoundMaxTiles)
+
+
+def setup_world_bounds(index, group: Optional[dist.ProcessGroup] = None, stream=None) -> bool:
+    """The one-collective protocol's setup (include/bm25mi.h,
+    bm25_search_shard_device): every rank exports its shard's tile bounds, the
+    ranks all-gather them once, and each rank's handle keeps the world's
+    [W, n_terms, stride] table, so a search takes the whole collection's
+    tile-bound threshold without the per-batch key exchange.  Collective:
+    every rank calls it; False (on every rank) when a shard keeps no tile
+    bounds or the collection has more tiles than one block selects over
+    (config 5: the two-exchange protocol stays).  ~2 GB per rank at config 3."""
+    world = dist.get_world_size(group)
+    info = index.info()
+    dev = torch.device("cuda", index.device)
+    backend = dist.get_backend(group)
+    tdev = "cpu" if backend == "gloo" else dev
+    # (no bounds anywhere -> 1, widest stride) by one MAX all-reduce; tiles by a SUM
+    t = torch.tensor([0 if info["tile_bounds"] else 1, index.bounds_stride()], dtype=torch.int64,
+                     device=tdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    n = torch.tensor([int(info["n_tiles"])], dtype=torch.int64, device=tdev)
+    dist.all_reduce(n, group=group)
+    missing, stride, tiles = int(t[0].item()), int(t[1].item()), int(n.item())
+    if missing or world * stride > BOUND_MAX_TILES + 4 * world or tiles < 1:
+        return False
+    local = torch.empty((index.n_terms, stride), dtype=torch.int16, device=dev)
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    index.bounds_export(local, stride, st)
+    with torch.cuda.stream(st):
+        g = _all_gather(local, group)  # [W, n_terms, stride]
+    st.synchronize()
+    index.set_world_bounds(g, world, stride, tiles)
+    return True
+
+
 def gather_keys(keys: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
     """All ranks' [Q, S] sample keys -> [W, Q, S] (rank-major), on every rank."""
     return _all_gather(keys, group)
@@ -252,6 +288,19 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
         stream = torch.cuda.current_stream(d_queries.device)
     elif not isinstance(stream, torch.cuda.Stream):
         stream = torch.cuda.ExternalStream(int(stream), device=d_queries.device)
+    if (merge is None and exchange is None and parts <= 1 and cuda
+            and index.__dict__.get("_bm25_world_bounds") is not None):
+        # one collective: the shard's keys >= the collection's threshold (its
+        # own from the world bounds), all-gathered and merged
+        with torch.cuda.stream(stream):
+            Q = d_queries.shape[0]
+            pk = torch.empty((2, Q, k), dtype=torch.int32, device=d_queries.device)
+            index.search_shard_device(d_queries, k, pk[0], pk[1].view(torch.float32), stream)
+            g = _all_gather(pk, group) if world > 1 else pk.unsqueeze(0)
+            from .index import merge_sorted_device
+            merge_sorted_device(d_queries.device.index, g, g[:, 1].view(torch.float32), world, Q,
+                                k, 2 * Q * k, d_docs, d_scores, stream)
+            return d_docs, d_scores
     if parts > 1 and merge is None and exchange is None:
         return _search_parts(index, d_queries, k, shard_docs_max, d_docs, d_scores, stream,
                              group, world, S, parts)

@@ -200,6 +200,41 @@ class GpuIndex:
             ctypes.c_void_p(d_docs.data_ptr()), ctypes.c_void_p(d_scores.data_ptr()),
             *[ctypes.c_void_p(x) for x in ss]))
 
+    # ------------------------------- doc-sharded, one collective (world bounds)
+    def bounds_stride(self) -> int:
+        """u16 per row of this index's tile bounds (its tiles rounded up to 4)."""
+        return (int(self.info()["n_tiles"]) + 3) // 4 * 4
+
+    def bounds_export(self, d_out, stride: int, stream=None) -> None:
+        """This index's tile bounds into d_out (a torch int16 [n_terms, stride]
+        device tensor; bm25_index_bounds_export)."""
+        s = getattr(stream, "cuda_stream", stream) or 0
+        check(lib.bm25_index_bounds_export(self._h, ctypes.c_void_p(d_out.data_ptr()), int(stride),
+                                           ctypes.c_void_p(s)))
+
+    def set_world_bounds(self, d_world, world: int, stride: int, world_tiles: int) -> None:
+        """Every shard's tile bounds ([world, n_terms, stride] int16 on this
+        device, kept referenced here) for bm25_search_shard_device; None clears."""
+        if d_world is None:
+            check(lib.bm25_index_set_world_bounds(self._h, None, 0, 0, 0))
+            self.__dict__.pop("_bm25_world_bounds", None)
+            return
+        check(lib.bm25_index_set_world_bounds(self._h, ctypes.c_void_p(d_world.data_ptr()),
+                                              int(world), int(stride), int(world_tiles)))
+        self._bm25_world_bounds = d_world
+        for f in self.__dict__.get("_bm25_forks", []):
+            f.set_world_bounds(d_world, world, stride, world_tiles)
+
+    def search_shard_device(self, d_queries, k: int, d_docs, d_scores, stream=None) -> None:
+        """This shard's keys >= the collection's threshold (world bounds) as an
+        unsorted padded [Q, k] list for the W-way merge (bm25_search_shard_device)."""
+        Q, T = d_queries.shape
+        s = getattr(stream, "cuda_stream", stream) or 0
+        check(lib.bm25_search_shard_device(self._h, ctypes.c_void_p(d_queries.data_ptr()), Q, T,
+                                           int(k), ctypes.c_void_p(d_docs.data_ptr()),
+                                           ctypes.c_void_p(d_scores.data_ptr()),
+                                           ctypes.c_void_p(s)))
+
     def scores_dense(self, query) -> np.ndarray:
         """All n_docs fp32 scores of one query (zero for untouched docs)."""
         q = np.ascontiguousarray(np.asarray(query).ravel(), dtype=np.int32)

@@ -405,8 +405,10 @@ void alloc_report(bm25_index* h) {
 }
 
 // Device pipeline on stream st; caller holds h->mu and has set the device.
+// shard: bm25_search_shard_device — the collection's threshold from the
+// world bounds and this shard's keys >= it, unsorted, for the W-way merge.
 int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, int k,
-               int32_t* d_docs, float* d_scores, hipStream_t st) {
+               int32_t* d_docs, float* d_scores, hipStream_t st, bool shard = false) {
   if (Q == 0 || k == 0) return BM25_OK;
   if (k > kMaxK) {  // any k up to n_docs: the large-k path (bm25mi_large.hip)
     // the list path when it applies (no dense score rows), else dense rows
@@ -462,15 +464,15 @@ int run_search(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T, in
   HIP_TRY(order_ws(h, st), "workspace order");
   h->large_fallback = 0;  // (counter [5] belongs to the last search: no large-k rows here)
   choose_theta_source(h);
-  const int P = search_geom(h->ix, h->ix.ntiles, k, 1, T).P;
+  const int P = shard_geom_world(h->ix, k, T, shard).P;
   h->ix.disp = Dispatch{};
   h->ix.disp.sample_p = P;
   arm_report(h, P, Q);
   EventPair* ev = next_events(h);
   if (ev) HIP_TRY(hipEventRecord(ev->a, st), "hipEventRecord");
-  HIP_TRY(launch_score(h->ix, d_queries, Q, T, k, h->ws, st), "score launch");
+  HIP_TRY(launch_score(h->ix, d_queries, Q, T, k, h->ws, st, shard), "score launch");
   if (ev) HIP_TRY(hipEventRecord(ev->b, st), "hipEventRecord");
-  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, P, h->ws, d_docs, d_scores, st),
+  HIP_TRY(launch_select(h->ix, d_queries, Q, T, k, P, h->ws, d_docs, d_scores, st, shard),
           "select launch");
   HIP_TRY(record_end(h, ev, st), "hipEventRecord");
   if (h->prof) {
@@ -791,6 +793,67 @@ int bm25_search_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
   return run_search(h, d_queries, Q, T, k, d_docs, d_scores, (hipStream_t)stream);
+}
+
+int bm25_index_bounds_export(bm25_index* h, uint16_t* d_out, int64_t stride, void* stream) {
+  if (!h || !d_out) return fail(BM25_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->ix.bmax)
+    return fail(BM25_EINVAL, "the index keeps no tile bounds (a dense, non-negative index does)");
+  const int64_t bs = bmax_stride(h->ix.ntiles);
+  if (stride < bs || stride % 4 != 0)
+    return fail(BM25_EINVAL, "stride %lld: a multiple of 4, >= %lld", (long long)stride, (long long)bs);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  const hipStream_t st = (hipStream_t)stream;
+  const int64_t V = h->ix.n_terms;
+  if (V == 0) return BM25_OK;
+  if (stride > bs) HIP_TRY(hipMemsetAsync(d_out, 0, sizeof(uint16_t) * V * stride, st), "hipMemsetAsync");
+  if (bs > 0)
+    HIP_TRY(hipMemcpy2DAsync(d_out, sizeof(uint16_t) * stride, h->ix.bmax, sizeof(uint16_t) * bs,
+                             sizeof(uint16_t) * bs, V, hipMemcpyDeviceToDevice, st),
+            "hipMemcpy2DAsync");
+  return BM25_OK;
+}
+
+int bm25_index_set_world_bounds(bm25_index* h, const uint16_t* d_world, int32_t world,
+                                int64_t stride, int64_t world_tiles) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!d_world) {
+    h->ix.wbmax = nullptr;
+    h->ix.wW = 0;
+    h->ix.wstride = h->ix.wtiles = 0;
+    return BM25_OK;
+  }
+  if (!h->ix.bmax)
+    return fail(BM25_EINVAL, "the index keeps no tile bounds (a dense, non-negative index does)");
+  if (world < 1 || stride % 4 != 0 || stride < bmax_stride(h->ix.ntiles) || world_tiles < 1 ||
+      world_tiles > (int64_t)world * stride)
+    return fail(BM25_EINVAL, "bad world bounds (world %d, stride %lld, tiles %lld)", world,
+                (long long)stride, (long long)world_tiles);
+  if ((int64_t)world * stride > kBoundMaxTiles + 4 * (int64_t)world)
+    return fail(BM25_EINVAL, "world bounds of %lld tiles exceed the %lld one block selects over",
+                (long long)((int64_t)world * stride), (long long)kBoundMaxTiles);
+  h->ix.wbmax = d_world;
+  h->ix.wW = world;
+  h->ix.wstride = stride;
+  h->ix.wtiles = world_tiles;
+  return BM25_OK;
+}
+
+int bm25_search_shard_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T,
+                             int32_t k, int32_t* d_docs, float* d_scores, void* stream) {
+  if (!h) return fail(BM25_EINVAL, "NULL index");
+  if (Q < 0 || T < 0) return fail(BM25_EINVAL, "negative query shape");
+  int rc = check_k(h, k, true);
+  if (rc) return rc;
+  if (Q == 0 || k == 0) return BM25_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->ix.wbmax) return fail(BM25_EINVAL, "no world bounds: bm25_index_set_world_bounds first");
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  h->sampled = false;
+  // k > 4096: this shard's exact top-k (padded past its documents)
+  return run_search(h, d_queries, Q, T, k, d_docs, d_scores, (hipStream_t)stream, k <= kMaxK);
 }
 
 int bm25_max_token_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T,

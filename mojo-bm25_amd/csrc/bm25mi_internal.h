@@ -134,6 +134,15 @@ struct DevIndex {
   // an index whose terms weigh alike); set by the host per search
   // (bm25mi_capi.cpp: bound_ok), read by search_geom
   bool bound_weak = false;
+  // World tile bounds of a doc-sharded collection (bm25_index_set_world_
+  // bounds): every shard's bmax rows, [wW][V][wstride] (a caller-owned device
+  // buffer, zero past each shard's tiles), so a shard's search
+  // (bm25_search_shard_device) takes the whole collection's tile-bound
+  // threshold by itself — no key exchange; wtiles = the collection's tiles
+  const uint16_t* wbmax = nullptr;
+  int32_t wW = 0;
+  int64_t wstride = 0;
+  int64_t wtiles = 0;
   SearchOpts opt;
   mutable Dispatch disp;  // written by the launchers (callers hold the handle's mutex)
 };
@@ -239,8 +248,13 @@ hipError_t launch_fill_tiles(const DevIndex& ix, const int32_t* d_indices, hipSt
 int64_t seg_entries(const DevIndex& ix, int64_t Q, int64_t T);
 // Score pass of a single-index search: SAMPLE + theta + REST (or the exact
 // pass when the index is too small to sample).
+// The threshold geometry of a search; world (a shard with world bounds): the
+// collection's tile-bound threshold when it serves (P = 0), else the shard's own.
+SampleGeom shard_geom_world(const DevIndex& ix, int k, int64_t T, bool world);
+// world: the threshold from the world tile bounds (ix.wbmax; a shard's
+// search for the W-way merge), else from this index's own.
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
-                        int k, const Workspace& ws, hipStream_t stream);
+                        int k, const Workspace& ws, hipStream_t stream, bool world = false);
 // The same in two halves for W doc shards searched together: each shard's
 // sample keys [Q][g.S] -> (all-gather across shards) -> theta over [W][Q][g.S]
 // + REST.

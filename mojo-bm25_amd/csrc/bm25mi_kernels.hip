@@ -1795,6 +1795,67 @@ __global__ __launch_bounds__(256) void build_bmax_kernel(const int64_t* __restri
 // in flight, coalesced over consecutive tiles: T * ntiles * 2 B per query);
 // wave 0 then selects and writes from LDS.
 constexpr int kBoundNT = 256;
+
+// The k-th largest of the block's u16 values (lbq: four per u64 group, nq4
+// groups, zero padding) and its rank among the values equal to it (need):
+// two 8-bit radix passes, each an LDS histogram of the digit (high byte, then
+// the low byte of the values in the chosen high bin) and one wave's scan of
+// it from the top bin down — four barriers, where a bit-by-bit selection
+// takes sixteen.  k >= 1; every thread returns the same (v, need).
+__device__ __forceinline__ void block_kth_u16(const uint64_t* lbq, int32_t nq4, uint32_t k,
+                                              uint32_t* hist, uint32_t* sh, uint32_t& v,
+                                              uint32_t& need) {
+  const uint32_t lane = lane_id();
+  uint32_t hi = 0u, nd = k;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int i = (int)threadIdx.x; i < 256; i += kBoundNT) hist[i] = 0u;
+    __syncthreads();
+    for (int32_t g = (int32_t)threadIdx.x; g < nq4; g += kBoundNT) {
+      const uint64_t x = lbq[g];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t val = (uint32_t)(x >> (16 * u)) & 0xFFFFu;
+        if (pass == 0) atomicAdd(&hist[val >> 8], 1u);
+        else if ((val >> 8) == hi) atomicAdd(&hist[val & 255u], 1u);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      // lane l holds bins 255 - 4l .. 252 - 4l (from the top)
+      uint32_t c[4], t = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = hist[255 - 4 * (int)lane - j];
+        t += c[j];
+      }
+      uint32_t above = wave_incl_scan(t) - t;  // values in the bins above this lane's
+      uint32_t bin1 = 0u, rk = 0u;              // (bin + 1, rank in it) of the k-th value
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (above < nd && nd <= above + c[j]) {
+          bin1 = 256u - 4u * lane - (uint32_t)j;
+          rk = nd - above;
+        }
+        above += c[j];
+      }
+      bin1 = wave_max_u32(bin1);
+      rk = wave_max_u32(rk);
+      if (lane == 0) {
+        sh[0] = bin1;
+        sh[1] = rk;
+      }
+    }
+    __syncthreads();
+    const uint32_t b = sh[0] - 1u;  // (fewer than k values cannot happen: padding counts)
+    nd = sh[1];
+    hi = pass == 0 ? b : hi;
+    v = pass == 0 ? (b << 8) : (v | b);
+    __syncthreads();  // (hist and sh are rewritten by the next pass)
+  }
+  need = nd;
+}
+
 __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
                                                               const uint16_t* __restrict__ bmax,
                                                               const int32_t* __restrict__ queries,
@@ -1802,12 +1863,18 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
                                                               uint64_t* __restrict__ keys,
                                                               uint64_t* __restrict__ theta,
                                                               int32_t* __restrict__ list_cnt,
-                                                              int32_t* __restrict__ counters) {
+                                                              int32_t* __restrict__ counters,
+                                                              int32_t nranks, int64_t wstride) {
   extern __shared__ uint64_t lbq[];  // lb_j as u16, four tiles per u64 (zero past the last)
   const int64_t q = blockIdx.x;
-  const int32_t nt = (int32_t)a.ntiles;
-  const int32_t nq4 = (nt + 3) >> 2;      // u64 groups of four tiles
-  const int64_t bs = bmax_stride(a.ntiles);  // a row holds whole groups (zero-padded)
+  // world bounds (nranks > 0, theta mode): the rows of every shard, [nranks][V]
+  // [wstride] — the groups of shard w follow those of shard w - 1 (a shard's
+  // zero padding holds no positive tile); otherwise this index's [V][bs]
+  const bool world = nranks > 0;
+  const int64_t bs = world ? wstride : bmax_stride(a.ntiles);  // a row holds whole groups
+  const int32_t gpr = (int32_t)(bs >> 2);                        // u64 groups per row
+  const int32_t nq4 = world ? nranks * gpr : (int32_t)((a.ntiles + 3) >> 2);
+  const int64_t rrank = world ? a.V * (bs >> 2) : 0;             // u64 between two shards' rows
   // the query's terms (T <= kBoundMaxTerms, launch_sample checks), loaded at uniform
   // addresses with every lane active; padding and ids >= V: none
   const int32_t* qt = queries + q * T;
@@ -1820,9 +1887,11 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
     row[i] = reinterpret_cast<const uint64_t*>(bmax + (has[i] ? (int64_t)t * bs : 0));
   }
   for (int32_t g = (int32_t)threadIdx.x; g < nq4; g += kBoundNT) {
+    const int32_t w = world ? g / gpr : 0;
+    const int64_t o = (int64_t)w * rrank + (g - w * gpr);
     uint64_t v[kBoundMaxTerms];
 #pragma unroll
-    for (int i = 0; i < (int)kBoundMaxTerms; ++i) v[i] = has[i] ? row[i][g] : 0ull;
+    for (int i = 0; i < (int)kBoundMaxTerms; ++i) v[i] = has[i] ? row[i][o] : 0ull;
     uint64_t m = 0ull;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1835,99 +1904,34 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
   }
   __syncthreads();
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  __shared__ uint32_t wtot[2][kBoundNT / 64];  // per-wave partials (double-buffered)
   if (theta != nullptr) {
     // a single-index search (theta != null, S = k): theta itself — the k-th
     // key in this index's own doc frame — and the resets theta_wave_kernel
     // would do (list count, search counters); no key list
     if (blockIdx.x == 0 && threadIdx.x < kCounters) counters[threadIdx.x] = 0;
-    uint32_t vk = 0u, needk = (uint32_t)S;
-    for (int bit = 15; bit >= 0; --bit) {
-      const uint32_t hm = (0xFFFFu << bit) & 0xFFFFu, cand = vk | (1u << bit);
-      uint32_t c = 0u;
-      for (int32_t g = (int32_t)threadIdx.x; g < nq4; g += kBoundNT) {
-        const uint64_t x = lbq[g];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) c += (((uint32_t)(x >> (16 * u)) & hm) == cand);
-      }
-      c = wave_sum_u32(c);
-      if (lane == 0) wtot[bit & 1][wv] = c;
-      __syncthreads();
-      uint32_t tot = 0u;
-#pragma unroll
-      for (int w = 0; w < kBoundNT / 64; ++w) tot += wtot[bit & 1][w];
-      if (tot >= needk) vk = cand;
-      else needk -= tot;
-    }
-    if (vk == 0u) {  // fewer than k positive tiles: every positive doc + zero fill
-      if (threadIdx.x == 0) {
+    __shared__ uint32_t hist[256], sh[2];
+    uint32_t vk = 0u, needk = 0u;
+    block_kth_u16(lbq, nq4, (uint32_t)S, hist, sh, vk, needk);
+    if (threadIdx.x == 0) {
+      if (vk == 0u) {  // fewer than k positive tiles: every positive doc + zero fill
         theta[q] = (uint64_t)0x80800000u << 32;  // kZeroFillTheta
-        list_cnt[q] = 0;
+      } else {
+        // the weakest key at the k-th bound's score: k tiles hold a document
+        // scoring at least vk, so k keys are >= it (the tie's doc does not
+        // tighten it: a doc scoring exactly an f16 value is rare)
+        _Float16 h;
+        const uint16_t xb = (uint16_t)vk;
+        __builtin_memcpy(&h, &xb, 2);
+        theta[q] = (uint64_t)score_key((float)h) << 32;
       }
-      return;
-    }
-    // the needk-th tile at vk in tile order holds the k-th key
-    __shared__ uint32_t wsk[kBoundNT / 64];
-    uint32_t seen = 0u;
-    for (int32_t g0 = 0; g0 < nq4; g0 += kBoundNT) {
-      const int32_t g = g0 + (int32_t)threadIdx.x;
-      const uint64_t x = g < nq4 ? lbq[g] : 0ull;
-      uint32_t ne = 0u;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) ne += ((uint32_t)(x >> (16 * u)) & 0xFFFFu) == vk;
-      const uint32_t ie = wave_incl_scan(ne);
-      if (lane == 63) wsk[wv] = ie;
-      __syncthreads();
-      uint32_t base = seen, tot = 0u;
-#pragma unroll
-      for (int w = 0; w < kBoundNT / 64; ++w) {
-        base += w < (int)wv ? wsk[w] : 0u;
-        tot += wsk[w];
-      }
-      uint32_t r = base + ie - ne;  // ties before this thread's first tile
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (((uint32_t)(x >> (16 * u)) & 0xFFFFu) == vk) {
-          if (r + 1u == needk) {
-            const int64_t j = 4 * (int64_t)g + u;
-            const int64_t last = min((j + 1) << S_log2, a.n_docs) - 1;  // (own doc frame)
-            _Float16 h;
-            const uint16_t xb = (uint16_t)vk;
-            __builtin_memcpy(&h, &xb, 2);
-            theta[q] = ((uint64_t)score_key((float)h) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)last);
-            list_cnt[q] = 0;
-          }
-          ++r;
-        }
-      }
-      seen += tot;
-      if (seen >= needk) return;  // (uniform: every thread saw the same totals)
-      __syncthreads();  // (wsk is rewritten by the next round)
+      list_cnt[q] = 0;
     }
     return;
   }
-  // the k-th largest lb (k = S), bit by bit from the top: a bit of the answer
-  // is set iff at least `need` values match its prefix with that bit set
-  // (padding tiles hold 0: they never match a set bit); every thread counts
-  // its groups, the waves' counts meet in LDS (one barrier per bit)
-  uint32_t v = 0u, need = (uint32_t)S;
-  for (int bit = 15; bit >= 0; --bit) {
-    const uint32_t hm = (0xFFFFu << bit) & 0xFFFFu, cand = v | (1u << bit);  // (16-bit values)
-    uint32_t c = 0u;
-    for (int32_t g = (int32_t)threadIdx.x; g < nq4; g += kBoundNT) {
-      const uint64_t x = lbq[g];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) c += (((uint32_t)(x >> (16 * u)) & hm) == cand);
-    }
-    c = wave_sum_u32(c);
-    if (lane == 0) wtot[bit & 1][wv] = c;
-    __syncthreads();
-    uint32_t tot = 0u;
-#pragma unroll
-    for (int w = 0; w < kBoundNT / 64; ++w) tot += wtot[bit & 1][w];
-    if (tot >= need) v = cand;
-    else need -= tot;
-  }
+  // the S-th largest lb and how many of the tiles at it are kept
+  __shared__ uint32_t hist[256], sh[2];
+  uint32_t v = 0u, need = 0u;
+  block_kth_u16(lbq, nq4, (uint32_t)S, hist, sh, v, need);
   // fewer than k positive tiles (v = 0): every positive one, zeros after it.
   // Otherwise the tiles above v and the first `need` tiles at v (lowest tile
   // first: their keys are the larger ones), compacted in tile order: rounds
@@ -2572,9 +2576,66 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
     key[j] = x >= th ? x : 0ull;  // (every list key is >= theta; key 0 = empty)
   }
   uint32_t n = 0;
-  if (!sg.unsorted && R <= 4) {
+  if (sg.unsorted) {
+    // a doc shard's list for the W-way merge: at most k keys go out as they
+    // are, padding after them
+#pragma unroll
+    for (int j = 0; j < R; ++j) n += key[j] != 0ull;
+    if (wave_sum_u32(n) <= (uint32_t)k) {
+      uint32_t base = 0u;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const bool keep = key[j] != 0ull;
+        const uint64_t b = __ballot(keep);
+        if (keep) {
+          const uint32_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+          docs[q * k + i] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)key[j]) + doc_offset);
+          scores[q * k + i] = key_score((uint32_t)(key[j] >> 32));
+        }
+        base += (uint32_t)__popcll(b);
+      }
+      for (int i = (int)base + (int)lane; i < k; i += 64) {
+        docs[q * k + i] = -1;
+        scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
+      }
+      return;
+    }
+    n = 0;
+  }
+  if (R == 8 && k <= 128) {  // (also at R = 16 the kernel spills)
+    // a longer list: a provisional threshold t1 from a sample (the list's
+    // first 128 keys, sorted in registers: the sample key at the rank where
+    // ~1.5 k of the list's keys are expected at or above it); when k to 256
+    // keys reach t1 — they hold the top k — those are compacted into LDS and
+    // sorted; otherwise the exact selection below
+    uint64_t smp[2] = {key[0], key[1]};
+    wave_sort_regs<2>(smp);
+    const int r = min(127, max(0, (int)((3u * (uint32_t)k * 64u) / (uint32_t)cnt)));
+    const uint64_t t1 = __shfl(r >= 64 ? smp[1] : smp[0], r & 63, 64);  // (no dynamic index)
+    uint32_t c = 0u;
+#pragma unroll
+    for (int j = 0; j < R; ++j) c += key[j] != 0ull && key[j] >= t1;
+    c = wave_sum_u32(c);
+    if (t1 != 0ull && c >= (uint32_t)k && c <= 256u) {
+      uint32_t base = 0u;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const bool keep = key[j] != 0ull && key[j] >= t1;
+        const uint64_t b = __ballot(keep);
+        if (keep)
+          keys[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
+        base += (uint32_t)__popcll(b);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      regs_sort_write<4>(keys, base, k, doc_offset, q, docs, scores);
+      return;
+    }
+  }
+  if (R <= 4) {
     // a list of <= 256 keys: sorted whole in registers, its first k written
-    // (no selection)
+    // (no selection; a shard's unsorted list may be sorted too)
     wave_sort_regs<R>(key);
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -2592,28 +2653,6 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
     return;
   }
   const uint64_t kth = wave_kth_key<R>(key, k, n);
-  if (sg.unsorted) {
-    // a doc shard's list for the W-way merge: the n kept keys in list order
-    // straight to the output, padding after them
-    uint32_t base = 0u;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const bool keep = key[j] != 0ull && key[j] >= kth;
-      const uint64_t b = __ballot(keep);
-      if (keep) {
-        const uint32_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-        docs[q * k + i] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)key[j]) + doc_offset);
-        scores[q * k + i] = key_score((uint32_t)(key[j] >> 32));
-      }
-      base += (uint32_t)__popcll(b);
-    }
-    for (int i = (int)base + (int)lane; i < k; i += 64) {
-      docs[q * k + i] = -1;
-      scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
-    }
-    return;
-  }
   // the n kept keys (>= kth; unique: doc ids differ) -> LDS, sorted best first
   uint32_t base = 0u;
 #pragma unroll
@@ -2912,10 +2951,15 @@ __global__ __launch_bounds__(64 * kQW) void merge_fast_kernel(Stage sg, int32_t 
     }
     return;
   }
-  if (cnt > 64 * kFastR && long_merge_one(sg, k, doc_offset, q, cnt, keys,
-                                           hist[threadIdx.x >> 6], docs, scores))
+  // a list of more than 1024 keys at k <= 128 (a few queries whose threshold
+  // sits far below their k-th key): merge_tail_kernel's block merge, whose
+  // 1024 threads load it in one round (block_long_merge); one wave alone
+  // kept the whole merge waiting ~20 us for such a query
+  const bool block_long = cnt > 1024 && k <= 128 && th != kZeroFillTheta;
+  if (!block_long && cnt > 64 * kFastR &&
+      long_merge_one(sg, k, doc_offset, q, cnt, keys, hist[threadIdx.x >> 6], docs, scores))
     return;
-  if (cnt > 64 * kFastR || (th == kZeroFillTheta && cnt < k)) {
+  if (block_long || cnt > 64 * kFastR || (th == kZeroFillTheta && cnt < k)) {
     if (lane == 0) ws.slow[atomicAdd(ws.counters + 4, 1)] = (int32_t)q;
     return;
   }
@@ -2965,6 +3009,76 @@ __global__ __launch_bounds__(kMergeNT) void merge_final_kernel(
   }
 }
 
+// A long list (1024 < cnt <= kMergeP keys, k <= 128, a threshold other than
+// zero fill) with the whole block: every thread loads its <= 8 keys in one
+// round; wave 0 sorts a 256-key sample of the list (its first 256 keys) in
+// registers and takes as provisional threshold t1 the sample key at the rank
+// where ~1.5 k of the list's keys are expected at or above it; when k to 256
+// keys reach t1 (they hold the top k) they are compacted into LDS and wave 0
+// sorts and writes them.  Returns false (nothing written; uniform) otherwise:
+// the caller's block merge takes the query.
+constexpr int kLongPT = kMergeP / kMergeNT;  // keys per thread
+__device__ bool block_long_merge(const Stage& sg, int32_t k, int64_t doc_offset, int64_t q,
+                                 uint64_t* keys, int32_t* s_cnt, uint64_t* s_t1,
+                                 int32_t* __restrict__ docs, float* __restrict__ scores) {
+  const int32_t cnt = sg.list_cnt[q];
+  const uint64_t th = sg.theta[q];
+  if (cnt <= 1024 || cnt > kMergeP || k > 128 || th == kZeroFillTheta) return false;
+  const uint64_t* lst = sg.list + q * (int64_t)sg.C;
+  const uint32_t lane = lane_id();
+  uint64_t x[kLongPT];
+#pragma unroll
+  for (int i = 0; i < kLongPT; ++i) {
+    const int e = i * kMergeNT + (int)threadIdx.x;
+    const uint64_t v = e < cnt ? lst[e] : 0ull;
+    x[i] = v >= th ? v : 0ull;
+  }
+  if (threadIdx.x < 64) {
+    uint64_t smp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t v = lst[j * 64 + (int)lane];  // (cnt > 1024: all in the list)
+      smp[j] = v >= th ? v : 0ull;
+    }
+    wave_sort_regs<4>(smp);
+    const int r = min(255, (int)((3u * (uint32_t)k * 128u) / (uint32_t)cnt));
+    const uint64_t a0 = r < 128 ? smp[0] : smp[2], a1 = r < 128 ? smp[1] : smp[3];
+    const uint64_t t1 = __shfl((r & 64) ? a1 : a0, r & 63, 64);  // (no dynamic index)
+    if (lane == 0) {
+      *s_t1 = t1;
+      *s_cnt = 0;
+    }
+  }
+  __syncthreads();
+  const uint64_t t1 = *s_t1;
+  uint32_t c = 0u;
+#pragma unroll
+  for (int i = 0; i < kLongPT; ++i) c += x[i] != 0ull && x[i] >= t1;
+  c = wave_sum_u32(c);
+  if (lane == 0 && c) atomicAdd(s_cnt, (int32_t)c);
+  __syncthreads();
+  const int32_t tot = *s_cnt;
+  __syncthreads();  // (s_cnt is reset below)
+  if (t1 == 0ull || tot < k || tot > 256) return false;
+  if (threadIdx.x == 0) *s_cnt = 0;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kLongPT; ++i) {
+    const bool keep = x[i] != 0ull && x[i] >= t1;
+    const uint64_t m = __ballot(keep);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(s_cnt, (int)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (keep)
+      keys[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = x[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) regs_sort_write<4>(keys, (uint32_t)tot, k, doc_offset, q, docs, scores);
+  __syncthreads();  // (keys are reused by the block's next query)
+  return true;
+}
+
 // The tail of a sampled search, one launch whose queries are counted on the
 // device (usually none): (1) the queries merge_fast_kernel left (lists longer
 // than it holds, zero-fill thresholds), merged as merge_first does; (2) the
@@ -2988,11 +3102,14 @@ __global__ __launch_bounds__(kMergeNT) void merge_tail_kernel(
     __hip_atomic_store(ws.report, (int32_t)stage_nq(fb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.report + 1, ws.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  __shared__ uint64_t s_t1;
   const int64_t ns = stage_nq(sl);
   for (int64_t i = blockIdx.x; i < ns; i += gridDim.x) {
     __syncthreads();
-    merge_first_one(sl, k, maxflag, a.doc_offset, a.n_docs, ws, docs, scores,
-                    (int64_t)sl.qmap[i], keys, s_nflag, &s_cnt, zf_bits);
+    const int64_t qi = (int64_t)sl.qmap[i];
+    if (block_long_merge(sl, k, a.doc_offset, qi, keys, &s_cnt, &s_t1, docs, scores)) continue;
+    merge_first_one(sl, k, maxflag, a.doc_offset, a.n_docs, ws, docs, scores, qi, keys, s_nflag,
+                    &s_cnt, zf_bits);
   }
   const int64_t nf = stage_nq(fb);
   for (int64_t qi = blockIdx.x; qi < nf; qi += gridDim.x) {
@@ -3204,6 +3321,14 @@ SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W, int64_t
       ntiles <= kBoundMaxTiles && ntiles * std::max(W, 1) >= kBoundTilesPerK * (int64_t)k)
     return SampleGeom{0, 1, g.S, 1};
   return g;
+}
+
+SampleGeom shard_geom_world(const DevIndex& ix, int k, int64_t T, bool world) {
+  if (world && ix.wbmax != nullptr) {
+    const SampleGeom g = search_geom(ix, ix.wtiles, k, 1, T);
+    if (g.P == 0) return g;
+  }
+  return search_geom(ix, ix.ntiles, k, 1, T);
 }
 
 // Every resident workgroup slot of the current device (a multiple of 8, one
@@ -3523,7 +3648,7 @@ hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q
     hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT),
                        (size_t)(bmax_stride(ix.ntiles) * 2), stream, args_of(ix), ix.bmax,
                        d_queries, (int32_t)T, ix.tile_shift, g.S, keys, (uint64_t*)nullptr,
-                       (int32_t*)nullptr, (int32_t*)nullptr);
+                       (int32_t*)nullptr, (int32_t*)nullptr, 0, (int64_t)0);
     return hipGetLastError();
   }
 #define CALL(s) sample_s<s>(ix, d_queries, Q, T, g, keys, ws, stream)
@@ -3594,19 +3719,27 @@ bool large_list_supported(const DevIndex& ix, int64_t T, int64_t Q) {
 }
 
 hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q, int64_t T,
-                        int k, const Workspace& ws, hipStream_t stream) {
-  const SampleGeom g = search_geom(ix, ix.ntiles, k, 1, T);
+                        int k, const Workspace& ws, hipStream_t stream, bool world) {
+  world = world && ix.wbmax != nullptr;
+  // a shard with world bounds sizes its threshold geometry by the collection
+  // (shard_geom_world: its own geometry where the world's tile bounds do not
+  // serve — the shard's own k-th key is a valid, looser threshold)
+  const SampleGeom g = shard_geom_world(ix, k, T, world);
+  world = world && g.P == 0;
+  const int64_t ntg = world ? ix.wtiles : ix.ntiles;
   if (g.P == 0 && Q > 0 && ix.ntiles > 0) {
     // one index: the bound kernel selects theta itself (no key list, no theta
-    // kernel)
-    if (ix.bmax == nullptr || ix.ntiles > kBoundMaxTiles || Q > 0x7FFFFFFF || T > kBoundMaxTerms)
+    // kernel); world: the threshold of the whole collection, from every
+    // shard's bounds (the keys >= it of this shard go to the W-way merge)
+    if (ix.bmax == nullptr || ntg > kBoundMaxTiles || Q > 0x7FFFFFFF || T > kBoundMaxTerms)
       return hipErrorInvalidValue;
     if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, d_queries, Q, T, ws, stream);
     ix.disp.kernels |= kKBound;
-    hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT),
-                       (size_t)(bmax_stride(ix.ntiles) * 2), stream, args_of(ix), ix.bmax,
-                       d_queries, (int32_t)T, ix.tile_shift, (int64_t)k, (uint64_t*)nullptr,
-                       ws.theta, ws.list_cnt, ws.counters);
+    const size_t lds = world ? (size_t)(ix.wW * ix.wstride * 2) : (size_t)(bmax_stride(ix.ntiles) * 2);
+    hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT), lds, stream,
+                       args_of(ix), world ? ix.wbmax : ix.bmax, d_queries, (int32_t)T,
+                       ix.tile_shift, (int64_t)k, (uint64_t*)nullptr, ws.theta, ws.list_cnt,
+                       ws.counters, world ? ix.wW : 0, world ? ix.wstride : (int64_t)0);
 #define CALL(s) finish_s<s>(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream, true)
     BM25_SHIFT_DISPATCH(CALL)
 #undef CALL

@@ -168,6 +168,47 @@ int main() {
                        (int64_t)W, (int64_t)Q, (int64_t)S, k, d_theta, d_cnt, C, 1, (int64_t)0,
                        (int64_t)10000000, d_ctr);
   });
+  // merge_fast on lists of n keys per query (unsorted shard mode and sorted)
+  {
+    int32_t *d_fb, *d_nflag, *d_slow, *d_ctrs;
+    CK(hipMalloc(&d_fb, sizeof(int32_t) * Q));
+    CK(hipMalloc(&d_nflag, sizeof(int32_t) * Q));
+    CK(hipMalloc(&d_slow, sizeof(int32_t) * Q));
+    CK(hipMalloc(&d_ctrs, sizeof(int32_t) * 64));
+    std::vector<uint64_t> th(Q, 1ull << 32);
+    CK(hipMemcpy(d_theta, th.data(), sizeof(uint64_t) * Q, hipMemcpyHostToDevice));
+    for (int n : {30, 120, 231, 400}) {
+      std::vector<uint64_t> lst((size_t)Q * C, 0ull);
+      for (int q = 0; q < Q; ++q)
+        for (int i = 0; i < n; ++i)
+          lst[(size_t)q * C + i] = make_key(2.f + (float)(rng() % 100000) * 1e-4f,
+                                            (uint32_t)(rng() % 10000000));
+      CK(hipMemcpy(d_list, lst.data(), sizeof(uint64_t) * lst.size(), hipMemcpyHostToDevice));
+      std::vector<int32_t> hn(Q, n);
+      CK(hipMemcpy(d_cnt, hn.data(), sizeof(int32_t) * Q, hipMemcpyHostToDevice));
+      for (int uns = 0; uns < 2; ++uns) {
+        Stage sg{};
+        sg.theta = d_theta;
+        sg.list = d_list;
+        sg.list_cnt = d_cnt;
+        sg.C = C;
+        sg.fb = d_fb;
+        sg.fb_cnt = d_ctrs + 2;
+        sg.nq_host = Q;
+        sg.unsorted = uns != 0;
+        Workspace ws{};
+        ws.nflag = d_nflag;
+        ws.slow = d_slow;
+        ws.counters = d_ctrs;
+        char name[96];
+        snprintf(name, sizeof name, "merge_fast n=%d %s k=100", n, uns ? "unsorted" : "sorted");
+        time_it(name, [&] {
+          hipLaunchKernelGGL(merge_fast_kernel, dim3(Q / kQW), dim3(64 * kQW), 0, 0, sg, k,
+                             (int64_t)0, ws, d_od, d_os);
+        });
+      }
+    }
+  }
   CK(hipDeviceSynchronize());
   return 0;
 }

@@ -20,6 +20,10 @@ for step in ${STEPS:-tests lines}; do
     tail -1 $OUT/pytest_gpu.log
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; tail -20 $OUT/smoke.log; exit 1; }
     ;;
+  btrace)  # kernel trace + stats of one bench command: BARGS="--config c2 ..."
+    ( export TMPDIR=/tmp; cd /tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/btrace -o run -- python3 $R/bench.py $BARGS --cpu-queries 0 --e2e-batches 0 > $OUT/btrace.json 2> $OUT/btrace.err ) || { echo btrace failed; tail -5 $OUT/btrace.err; exit 1; }
+    ;;
   sel)  # selected GPU tests: TESTS="path::name ..."
     timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread > $OUT/pytest_sel.log 2>&1 || { echo "pytest sel failed"; grep -E "FAILED|Error|passed|failed" $OUT/pytest_sel.log | tail -30; exit 1; }
     tail -1 $OUT/pytest_sel.log

@@ -31,7 +31,9 @@ constants are stated in the output line.  Two ways to add them:
       2-replica x W/2-shard split, each rank Q/2 queries on a 2/W shard;
       PROBE_PIPE=2: two batches in flight per rank, on the handle and a fork
       with their own streams, collectives inline on one comm stream;
-      PROBE_LOCAL=1: each shard's own single-index top-k, one all-gather)
+      PROBE_LOCAL=1: each shard's own single-index top-k, one all-gather;
+      PROBE_WORLD=1: one collective — every shard holds the world's tile
+      bounds and takes the collection's threshold itself)
 """
 import json
 import os
@@ -276,6 +278,7 @@ def main():
     pipe = int(os.environ.get("PROBE_PIPE", "1"))  # batches in flight per rank
     gated = os.environ.get("PROBE_GATED") == "1"   # run_gated: two batches, threshold ahead
     nctx = int(os.environ.get("PROBE_STREAMS", "0"))  # run_streams with this many contexts
+    world_b = os.environ.get("PROBE_WORLD") == "1"  # one collective: world tile bounds
     gated = gated or nctx > 0
     w1_ms = None
     jobs = [(int(x), 1) for x in (sys.argv[1:] or ["1", "2", "4", "8"])]
@@ -334,7 +337,29 @@ def main():
                         keys_p.append(kk)
                         g_p.append(g)
                     torch.cuda.synchronize()
-                    if nctx > 0:
+                    if world_b:
+                        # one collective (bm25_search_shard_device): every shard
+                        # keeps the world's tile bounds; its lists into the packed
+                        # buffer as the list all-gather delivers them
+                        stride = max(x.bounds_stride() for x in shards)
+                        wb = torch.empty((W, cfg.n_terms, stride), dtype=torch.int16,
+                                         device="cuda")
+                        for r, ix_ in enumerate(shards):
+                            ix_.bounds_export(wb[r], stride, st)
+                        tiles = sum(int(x.info()["n_tiles"]) for x in shards)
+                        for ix_ in shards:
+                            ix_.set_world_bounds(wb, W, stride, tiles)
+                        gw = g_p[0]
+                        for r, ix_ in enumerate(shards):
+                            ix_.search_shard_device(q, k, gw[r, 0], gw[r, 1].view(torch.float32), st)
+                        torch.cuda.synchronize()
+
+                        def one(r):
+                            ix_ = shards[r]
+                            ix_.search_shard_device(q, k, gw[r, 0], gw[r, 1].view(torch.float32), st)
+                            merge_sorted_device(q.device.index, gw, gw[:, 1].view(torch.float32), W,
+                                                Q, k, 2 * Q * k, out_d, out_s, st)
+                    elif nctx > 0:
                         sforks = {}
                         sstreams = [torch.cuda.Stream() for _ in range(3)]
                         scomm = torch.cuda.Stream()
@@ -448,13 +473,18 @@ def main():
                 worst = max(x["ms"] for x in per_rank)
                 inline = inline or pipe > 1 or gated
                 coll_us = 0.0 if inline else (model_gather_us(list_b, W) if
-                                              os.environ.get("PROBE_LOCAL") == "1" else
+                                              (os.environ.get("PROBE_LOCAL") == "1" or
+                                               (world_b and W > 1)) else
                                               model_gather_us(keys_b, W) + model_gather_us(list_b, W))
                 proj = worst + coll_us * 1e-3
                 if W == 1 and P == 1 and R == 1 and gp == 100:
                     w1_ms = worst
                 line = {"W": W * R, "shards": W, "replicas": R, "parts": P, "grid_pct": gp,
                         "batches_in_flight": 2 if gated else (pipe if W > 1 else 1),
+                        "protocol": ("one collective: world tile bounds, shard lists, W-way "
+                                     "merge" if world_b and W > 1 else
+                                     "two collectives: key all-gather, theta, lists, merge"
+                                     if W > 1 else "single index"),
                         "pipeline": (f"three streams, {nctx} contexts (run_streams)" if nctx
                                      else "gated (run_gated)" if gated else None),
                         "queries_per_rank": Q, "shard_docs_max": smax, "sample_width": S,

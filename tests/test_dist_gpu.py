@@ -31,7 +31,7 @@ CASES = {
 }
 
 
-def _worker(rank, world, port, case, out, parts=1):
+def _worker(rank, world, port, case, out, parts=1, world_bounds=False):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -54,6 +54,9 @@ def _worker(rank, world, port, case, out, parts=1):
         d_scores = torch.empty((len(q), cfg.k), dtype=torch.float32, device="cuda")
         stream = torch.cuda.Stream()   # a non-current stream: the body must order on it
         merge = gpu_merge(0, stream) if os.environ.get("BM25_TEST_MERGE") == "sort" else None
+        if world_bounds:  # the one-collective protocol: the world's tile bounds on every rank
+            from bm25mi.dist import setup_world_bounds
+            assert setup_world_bounds(index)
         docs, scores = sharded_search(index, dq, cfg.k, sdm, d_docs, d_scores, merge, stream,
                                       parts=parts)
         if parts > 1:  # the parts ran on forks of the index, each on its own stream
@@ -80,12 +83,23 @@ def test_sharded_search_parts_real_process_group(gpu, tmp_path, world, case, par
     _run_case(tmp_path, world, case, parts)
 
 
-def _run_case(tmp_path, world, case, parts):
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", ["synth", "small"])
+def test_world_bounds_one_collective_real_process_group(gpu, tmp_path, world, case):
+    """The one-collective protocol (setup_world_bounds once, then per batch
+    bm25_search_shard_device + one all-gather of the lists + the W-way
+    merge) through real gloo groups: bit-exact vs the single-index oracle,
+    including shards smaller than k (padding)."""
+    _run_case(tmp_path, world, case, 1, True)
+
+
+def _run_case(tmp_path, world, case, parts, world_bounds=False):
     from bm25mi import synth
     from oracle import oracle
     cfg = synth.Config(*CASES[case])
     out = str(tmp_path / "r.npz")
-    mp.spawn(_worker, args=(world, _free_port(), case, out, parts), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), case, out, parts, world_bounds), nprocs=world,
+             join=True)
     got = np.load(out)
     q = synth.make_queries(cfg)
     q[2, 3:] = -1

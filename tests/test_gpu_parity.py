@@ -1120,10 +1120,75 @@ def test_config4_c3_index_eight_shards_full_batch(gpu):
     for lo, hi in bounds:
         shards.append(GpuIndex(*synth.make_index(cfg, lo, hi, threads=16), hi - lo, doc_offset=lo))
         _progress(f"c4: rank shard [{lo}, {hi}) built")
-    _exact(_protocol_search(shards, torch.from_numpy(q).cuda(), cfg.k, sdm), ref)
+    dq = torch.from_numpy(q).cuda()
+    _exact(_protocol_search(shards, dq, cfg.k, sdm), ref)
     d = shards[0].last_dispatch()
     assert d["kernels"] - {"bound_off"} == _want_kernels(
         _geom_p(shards[0], cfg.k, W, (sdm + 2047) // 2048, weak="bound_off" in d["kernels"])), d
+    _progress("c4: two-collective protocol bit-exact")
+    _exact(_world_bounds_search(shards, dq, cfg.k), ref)
+    assert "bound_keys" in shards[0].last_dispatch()["kernels"]
+    _progress("c4: one-collective protocol (world tile bounds) bit-exact")
+    for s in shards:
+        s.close()
+
+
+def _world_bounds_search(shards, dq, k):
+    """The one-collective protocol over doc shards held by this process: the
+    world's tile bounds stacked as their all-gather delivers them, each
+    shard's bm25_search_shard_device list in the packed [W, 2, Q, k] buffer
+    as the list all-gather delivers it, the W-way merge."""
+    import torch
+    from bm25mi.index import merge_sorted_device
+    W, Q = len(shards), dq.shape[0]
+    stride = max(s.bounds_stride() for s in shards)
+    wb = torch.empty((W, shards[0].n_terms, stride), dtype=torch.int16, device="cuda")
+    for r, s in enumerate(shards):
+        s.bounds_export(wb[r], stride)
+    tiles = sum(int(s.info()["n_tiles"]) for s in shards)
+    g = torch.empty((W, 2, Q, k), dtype=torch.int32, device="cuda")
+    for r, s in enumerate(shards):
+        s.set_world_bounds(wb, W, stride, tiles)
+        s.search_shard_device(dq, k, g[r, 0], g[r, 1].view(torch.float32))
+    md = torch.empty((Q, k), dtype=torch.int32, device="cuda")
+    ms = torch.empty((Q, k), dtype=torch.float32, device="cuda")
+    merge_sorted_device(0, g, g[:, 1].view(torch.float32), W, Q, k, 2 * Q * k, md, ms)
+    torch.cuda.synchronize()
+    for s in shards:
+        s.set_world_bounds(None, 0, 0, 0)
+    return md.cpu().numpy(), ms.cpu().numpy()
+
+
+def test_world_bounds_shards_ties_small_shards(gpu):
+    """bm25_search_shard_device with world tile bounds on uneven shards (40
+    tiles, 160 tiles, the rest): the collection's threshold taken by each
+    shard, quarter-step ties at it, zero-fill rows, k above a shard's tiles
+    and k > 4096 (each shard's exact top-k) — merged, bit-exact vs the
+    single-index oracle; without world bounds the entry point refuses."""
+    import scipy.sparse as sp
+    import torch
+    N, V = 600_000, 200
+    ip, ix, dt = _bound_case(91, N, V, 20)
+    rng = np.random.default_rng(6)
+    q = np.concatenate([rng.integers(0, 20, size=(24, 3)),
+                        rng.integers(20, V, size=(24, 3))], axis=1).astype(np.int32)
+    q[0, :] = -1
+    q[1, :] = -1
+    q[1, 0] = 20 + int(np.argmin(np.diff(ip)[20:]))  # a rare term: fewer than k positive docs
+    cuts = [0, 2048 * 40, 2048 * 200, N]
+    m = sp.csc_matrix((dt, ix, ip), shape=(N, V))
+    shards = []
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        s = m[lo:hi].tocsc()
+        s.sort_indices()
+        shards.append(_idx(s.indptr.astype(np.int64), s.indices.astype(np.int32),
+                           s.data.astype(np.float32), hi - lo, doc_offset=lo, segments="dense"))
+    dq = torch.from_numpy(q).cuda()
+    d = torch.empty((len(q), 10), dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError, match="world bounds"):
+        shards[0].search_shard_device(dq, 10, d, d.view(torch.float32))
+    for k in (1, 10, 16, 5000):
+        _exact(_world_bounds_search(shards, dq, k), oracle.search_c(N, ip, ix, dt, q, k, threads=8))
     for s in shards:
         s.close()
 
