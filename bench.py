@@ -218,6 +218,11 @@ def main():
                          "two all-gathers); replica = every rank holds the whole index and "
                          "searches its Q/N slice of the batch, no collective (SURVEY.md §8(e) "
                          "comparison point)")
+    ap.add_argument("--protocol", default="auto", choices=("auto", "one", "two"),
+                    help="N > 1 shard mode: one = every rank keeps the world's tile bounds "
+                         "(one all-gather at setup) and each batch needs ONE collective, the "
+                         "[Q, k] lists; two = the sample-key all-gather + theta + the lists; "
+                         "auto = one where the collection's tile bounds allow it")
     ap.add_argument("--parts", type=int, default=1,
                     help="N > 1 shard mode: pipeline each batch as this many row ranges over "
                          "forks of the rank's index on their own streams (bm25mi.dist."
@@ -308,6 +313,13 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     sdm = max(b - a for a, b in (synth.shard_bounds(cfg.n_docs, world, r) for r in range(world)))
+    one_coll = False
+    if world > 1 and not replica and args.protocol != "two" and args.parts <= 1:
+        from bm25mi.dist import setup_world_bounds
+        one_coll = setup_world_bounds(index)
+        if args.protocol == "one" and not one_coll:
+            raise SystemExit("--protocol one: the collection's tile bounds do not allow it")
+        log(f"[rank {rank}] doc-shard protocol: {'one collective (world tile bounds)' if one_coll else 'two collectives'}")
 
     def step():
         if world > 1 and not replica:  # global theta: RCCL all-gathers of sample keys and [Q, k] lists (bm25mi.dist)
@@ -449,8 +461,11 @@ def main():
                 "tile_docs": info["tile_docs"],
                 "parallelism": (f"replica x{world} (whole index per GPU, batch split, no "
                                 "collective)" if replica else f"doc-shard x{world}" + (
-                    f" + {'RCCL' if args.backend == 'nccl' else args.backend} all-gathers "
-                    "(sample keys, packed [Q, k] lists)" + (
+                    (f" + ONE {'RCCL' if args.backend == 'nccl' else args.backend} all-gather "
+                     "per batch (packed [Q, k] lists; every rank keeps the world's tile bounds, "
+                     "all-gathered once at setup)" if one_coll else
+                     f" + {'RCCL' if args.backend == 'nccl' else args.backend} all-gathers "
+                     "(sample keys, packed [Q, k] lists)") + (
                         f", batch pipelined as {args.parts} parts on forked contexts"
                         if args.parts > 1 else "") if world > 1 else "")),
                 "score_kernels": sorted(dispatch["kernels"]),

@@ -121,7 +121,8 @@ def _agree_width(index, S: int, k: int, device, group=None) -> None:
 BOUND_MAX_TILES = 30720  # tiles one block selects a threshold over (kBoundMaxTiles)
 
 
-def setup_world_bounds(index, group: Optional[dist.ProcessGroup] = None, stream=None) -> bool:
+def setup_world_bounds(index, group: Optional[dist.ProcessGroup] = None, stream=None,
+                       device=None) -> bool:
     """The one-collective protocol's setup (include/bm25mi.h,
     bm25_search_shard_device): every rank exports its shard's tile bounds, the
     ranks all-gather them once, and each rank's handle keeps the world's
@@ -132,7 +133,7 @@ def setup_world_bounds(index, group: Optional[dist.ProcessGroup] = None, stream=
     (config 5: the two-exchange protocol stays).  ~2 GB per rank at config 3."""
     world = dist.get_world_size(group)
     info = index.info()
-    dev = torch.device("cuda", index.device)
+    dev = torch.device(device) if device is not None else torch.device("cuda", index.device)
     backend = dist.get_backend(group)
     tdev = "cpu" if backend == "gloo" else dev
     # (no bounds anywhere -> 1, widest stride) by one MAX all-reduce; tiles by a SUM
@@ -145,11 +146,13 @@ def setup_world_bounds(index, group: Optional[dist.ProcessGroup] = None, stream=
     if missing or world * stride > BOUND_MAX_TILES + 4 * world or tiles < 1:
         return False
     local = torch.empty((index.n_terms, stride), dtype=torch.int16, device=dev)
-    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    st = (stream if stream is not None else torch.cuda.current_stream(dev)) if dev.type == "cuda" \
+        else None
     index.bounds_export(local, stride, st)
-    with torch.cuda.stream(st):
-        g = _all_gather(local, group)  # [W, n_terms, stride]
-    st.synchronize()
+    with _stream_ctx(st):  # (as int32 pairs: RCCL and gloo move no int16)
+        g = _all_gather(local.view(torch.int32), group).view(torch.int16)  # [W, n_terms, stride]
+    if st is not None:
+        st.synchronize()
     index.set_world_bounds(g, world, stride, tiles)
     return True
 
@@ -288,11 +291,11 @@ def sharded_search(index, d_queries: torch.Tensor, k: int, shard_docs_max: int,
         stream = torch.cuda.current_stream(d_queries.device)
     elif not isinstance(stream, torch.cuda.Stream):
         stream = torch.cuda.ExternalStream(int(stream), device=d_queries.device)
-    if (merge is None and exchange is None and parts <= 1 and cuda
+    if (merge is None and exchange is None and parts <= 1
             and index.__dict__.get("_bm25_world_bounds") is not None):
         # one collective: the shard's keys >= the collection's threshold (its
         # own from the world bounds), all-gathered and merged
-        with torch.cuda.stream(stream):
+        with _stream_ctx(stream):
             Q = d_queries.shape[0]
             pk = torch.empty((2, Q, k), dtype=torch.int32, device=d_queries.device)
             index.search_shard_device(d_queries, k, pk[0], pk[1].view(torch.float32), stream)

@@ -384,3 +384,111 @@ def test_gloo_search_parts_protocol(tmp_path, world, parts):
     cuts = [args[2] * i // parts for i in range(parts + 1)]
     sizes = [b - a for a, b in zip(cuts[:-1], cuts[1:])]
     assert list(got["calls"]) == sizes + sizes  # every sample half, then every finish half
+
+
+class _NumpyWorldShard(_NumpyShard):
+    """_NumpyShard with the one-collective protocol's calls (GpuIndex's
+    signatures): its tile bounds exported as f16 bits rounded down, the
+    world's bounds kept as all-gathered, and bm25_search_shard_device's
+    answer — the collection's threshold (the k-th best tile bound of the
+    world, as a score: the weakest key at it) and the shard's keys at or
+    above it (at most k, best first), zero fill with its smallest untouched
+    documents when the world has fewer than k positive tiles, padding doc -1
+    / score bits ~0."""
+
+    def __init__(self, *a, n_terms=0):
+        super().__init__(*a)
+        self.n_terms = n_terms
+        self.ntiles = (self.hi - self.lo + self.tile - 1) // self.tile
+
+    def info(self):
+        return {"tile_bounds": True, "n_tiles": self.ntiles}
+
+    def bounds_stride(self):
+        return (self.ntiles + 3) // 4 * 4
+
+    def bounds_export(self, out, stride, stream=None):
+        b = np.zeros((self.n_terms, stride), np.float32)
+        for t in range(self.n_terms):
+            a, e = int(self.ip[t]), int(self.ip[t + 1])
+            sel = (self.ix[a:e] >= self.lo) & (self.ix[a:e] < self.hi)
+            tiles = (self.ix[a:e][sel] - self.lo) // self.tile
+            np.maximum.at(b[t], tiles, self.dt[a:e][sel])
+        h = b.astype(np.float16)
+        h = np.where(h.astype(np.float32) > b, np.nextafter(h, np.float16(-np.inf)), h)
+        out.copy_(torch.from_numpy(h.view(np.int16)))
+
+    def set_world_bounds(self, g, world, stride, tiles):
+        self._bm25_world_bounds = g
+        self.world_tiles = tiles
+
+    def search_shard_device(self, q, k, d_docs, d_scores, stream=None):
+        self.calls.append(("shard", q.shape[0]))
+        wb = self._bm25_world_bounds.numpy().view(np.float16).astype(np.float32)  # [W, V, stride]
+        docs = np.full((q.shape[0], k), -1, np.int32)
+        scores = np.full((q.shape[0], k), -1, np.int32).view(np.float32)
+        for i, row in enumerate(q.numpy()):
+            terms = np.unique(row[row >= 0])
+            lb = wb[:, terms, :].max(axis=1).ravel() if terms.size else np.zeros(1, np.float32)
+            lb = np.sort(lb)[::-1]
+            s = self._dense(row)
+            if lb.size >= k and lb[k - 1] > 0:
+                sel = np.nonzero(s >= lb[k - 1])[0]
+                lst = sorted(((-float(s[d]), self.lo + int(d)) for d in sel))[:k]
+            else:  # every positive doc, then the smallest untouched ones at score 0
+                pos = sorted((-float(s[d]), self.lo + int(d)) for d in np.nonzero(s > 0)[0])
+                zero = [(0.0, self.lo + int(d)) for d in np.nonzero(s == 0)[0][:k]]
+                lst = (pos + zero)[:k]
+            for j, (ms, d) in enumerate(lst):
+                docs[i, j], scores[i, j] = d, -ms
+        d_docs.copy_(torch.from_numpy(docs))
+        d_scores.copy_(torch.from_numpy(scores))
+
+
+def _world_worker(rank, world, port, args, k, tile, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bm25mi.index as bi
+        from bm25mi.dist import setup_world_bounds, shard_bounds, sharded_search
+        bi.merge_sorted_device = _merge_packed_cpu  # the host stand-in of the HIP merge
+        N, V, Q, T, seed = args
+        ip, ix, dt, q = _tie_index(N, V, Q, T, seed)
+        lo, hi = shard_bounds(N, world, rank, align=tile)
+        sdm = max(b - a for a, b in (shard_bounds(N, world, r, align=tile) for r in range(world)))
+        shard = _NumpyWorldShard(ip, ix, dt, lo, hi, tile, (sdm + tile - 1) // tile, n_terms=V)
+        assert setup_world_bounds(shard, device="cpu")
+        wb = shard._bm25_world_bounds
+        assert tuple(wb.shape) == (world, V, shard.bounds_stride())
+        d = torch.zeros((Q, k), dtype=torch.int32)
+        s = torch.zeros((Q, k), dtype=torch.float32)
+        sharded_search(shard, torch.from_numpy(q), k, sdm, d, s, n_docs_total=N)
+        if rank == 0:
+            np.savez(result_path, docs=d.numpy(), scores=s.numpy(),
+                     calls=np.array([c[0] for c in shard.calls]),
+                     tiles=np.array([shard.world_tiles]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_world_bounds_one_collective(tmp_path, world):
+    """The one-collective protocol's plumbing through real gloo groups:
+    setup_world_bounds (the MAX/SUM agreement, the bounds all-gather), then per
+    batch one shard search, one all-gather of the packed lists and the merge —
+    the single-index top-k bit for bit on a tie-heavy index; no sample or
+    finish half runs."""
+    from oracle import oracle
+    args = (12000, 6, 7, 3, 11)
+    k, tile = 40, 256
+    out = str(tmp_path / "w.npz")
+    mp.spawn(_world_worker, args=(world, _free_port(), args, k, tile, out), nprocs=world,
+             join=True)
+    got = np.load(out)
+    ip, ix, dt, q = _tie_index(*args)
+    ref = oracle.search_c(args[0], ip, ix, dt, q, k)
+    assert np.array_equal(got["docs"], ref[0])
+    assert np.array_equal(got["scores"].view(np.uint32), ref[1].view(np.uint32))
+    assert list(got["calls"]) == ["shard"]
+    assert int(got["tiles"][0]) == (12000 + tile - 1) // tile or int(got["tiles"][0]) > 0
