@@ -423,6 +423,11 @@ int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
  *                    [2], [3]) — a kernel build of its own: the two counts'
  *                    registers cost the pass 13 % on an 8-way doc shard;
  *                    0 (default): not counted
+ *   "rest_split"     1: where the REST pass gives each resident wave few
+ *                    items (< 48: a doc shard of a few-GPU collection), a
+ *                    heavy query's 8-tile band is split into 2..8 items (a
+ *                    per-search table built by the threshold kernel);
+ *                    0 (default: measured no faster at W = 8)
  *   "grid_pct"       percent of the device's resident workgroup slots the
  *                    persistent score kernels launch (1..100, default 100):
  *                    below 100 leaves slots for kernels of another stream
@@ -442,7 +447,9 @@ int bm25_index_get_option(const bm25_index* idx, const char* name, int64_t* valu
  *                threshold was off for this search because earlier searches
  *                on the handle that used it overflowed their candidate lists
  *                (more than 1/16 of their queries took the exact fallback) —
- *                it is retried after 64, 128, ... 4096 searches
+ *                it is retried after 64, 128, ... 4096 searches; 512 (a
+ *                flag): REST counted its skipped postings (count_skips);
+ *                1024 (a flag): REST ran over split items (rest_split)
  *   *term_lanes  flat kernel: term lanes per tile (8, 16, 32 or 64)
  *   band_tiles   [3]: flat kernel tiles per item of ALL, SAMPLE, REST
  *   *sample_p    sampling stride of the search (1: exact pass, 0: tile-bound

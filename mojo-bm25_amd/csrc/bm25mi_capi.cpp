@@ -120,6 +120,10 @@ void free_ws(Workspace& ws) {
   hipFree(ws.slow);
   hipFree(ws.wctr);
   hipFree(ws.seg);
+  hipFree(ws.qw);
+  hipFree(ws.sub);
+  hipFree(ws.sub_ipb);
+  hipFree(ws.sub_done);
   ws = Workspace{};
 }
 
@@ -146,6 +150,7 @@ SearchOpts env_opts() {
   o.grid_pct = std::min(100, std::max(1, env_int("BM25_GRID_PCT", o.grid_pct)));
   o.count_skips = env_int("BM25_COUNT_SKIPS", o.count_skips) != 0;
   o.large_lists = env_int("BM25_LARGE_LISTS", o.large_lists) != 0;
+  o.rest_split = env_int("BM25_REST_SPLIT", o.rest_split) != 0;
   return o;
 }
 
@@ -184,6 +189,9 @@ int set_opt(SearchOpts& o, const char* name, int64_t v) {
   } else if (n == "large_lists") {
     if (v != 0 && v != 1) return fail(BM25_EINVAL, "large_lists must be 0 or 1");
     o.large_lists = (int)v;
+  } else if (n == "rest_split") {
+    if (v != 0 && v != 1) return fail(BM25_EINVAL, "rest_split must be 0 or 1");
+    o.rest_split = (int)v;
   } else if (n == "count_skips") {
     if (v != 0 && v != 1) return fail(BM25_EINVAL, "count_skips must be 0 or 1");
     o.count_skips = (int)v;
@@ -211,6 +219,7 @@ int get_opt(const SearchOpts& o, const char* name, int64_t* v) {
   else if (n == "grid_pct") *v = o.grid_pct;
   else if (n == "count_skips") *v = o.count_skips;
   else if (n == "large_lists") *v = o.large_lists;
+  else if (n == "rest_split") *v = o.rest_split;
   else return fail(BM25_EINVAL, "unknown option '%s'", name);
   return BM25_OK;
 }
@@ -256,6 +265,13 @@ int ensure_ws(bm25_index* h, int64_t Q, int64_t T, int k, hipStream_t st) {
   // claim counters start at 0; each flat launch's last wave re-zeroes its region
   HIP_TRY(hipMemsetAsync(ws.wctr, 0, sizeof(int32_t) * kWctrRegions * kWctrInts, st),
           "hipMemsetAsync(wctr)");
+  // the split-item table of the REST pass (bound_keys_kernel builds it; its
+  // finished-block count resets itself)
+  HIP_TRY(hipMalloc(&ws.qw, sizeof(uint32_t) * q), "hipMalloc(qw)");
+  HIP_TRY(hipMalloc(&ws.sub, sizeof(uint32_t) * q * 8), "hipMalloc(sub)");
+  HIP_TRY(hipMalloc(&ws.sub_ipb, sizeof(int32_t)), "hipMalloc(sub_ipb)");
+  HIP_TRY(hipMalloc(&ws.sub_done, sizeof(int32_t)), "hipMalloc(sub_done)");
+  HIP_TRY(hipMemsetAsync(ws.sub_done, 0, sizeof(int32_t), st), "hipMemsetAsync(sub_done)");
   ws.cap_seg = need_seg;
   if (ws.cap_seg > 0) HIP_TRY(hipMalloc(&ws.seg, sizeof(uint64_t) * ws.cap_seg), "hipMalloc(seg)");
   ws.list_cap = C;

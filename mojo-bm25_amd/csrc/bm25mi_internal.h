@@ -40,6 +40,8 @@ __host__ __device__ inline uint64_t make_key(float s, uint32_t doc) {
 constexpr int kTileM = 4;
 // Keys per sample tile of the large-k list path (the best of each 256-doc slice).
 constexpr int kLargeM = 8;
+constexpr int kSplitM = 3;  // the REST build over split items (bm25mi_kernels.hip)
+constexpr int kSplitItemsPerWave = 48;  // split REST items below this many items per wave
 // Largest k of the sampled-threshold pipeline; larger k (up to n_docs) take
 // the large-k path (bm25mi_large.hip).
 constexpr int kMaxK = 4096;
@@ -80,6 +82,7 @@ struct SearchOpts {
   int count_skips = 0;     // REST counts the postings its tile bound skips (a build of its own)
   int grid_pct = 100;      // percent of the resident slots the persistent score kernels take
   int large_lists = 1;     // k > kMaxK: the list path (0: dense score rows for every query)
+  int rest_split = 0;      // REST over split items where the waves get few items (measured: no gain)
 };
 
 // What the last search launched (bm25_search_dispatch).
@@ -91,6 +94,7 @@ enum {
   kKBoundOff = 256,  // (not a kernel) the tile-bound threshold was off for this search:
                      // earlier ones overflowed with it (DevIndex::bound_weak)
   kKCountSkips = 512,  // (a flag) REST counted the postings its tile bound skipped
+  kKRestSplit = 1024,  // (a flag) REST ran over split items (heavy queries' bands in pieces)
 };
 struct Dispatch {
   uint32_t kernels = 0;       // kK* bits of the score kernels launched
@@ -192,6 +196,13 @@ struct Workspace {
   int32_t* report = nullptr;     // host-mapped [2]: merge_tail_kernel writes the search's
                                  // fallback query count, then `seq` (null: no report)
   int32_t seq = 0;               // the search's sequence number on its handle
+  // split REST items (bound_keys_kernel builds the table per search): per
+  // query its weight, then the band's item table (<= 8 per query), the items
+  // per band, and the finished-block count of the build (self-resetting)
+  uint32_t* qw = nullptr;
+  uint32_t* sub = nullptr;
+  int32_t* sub_ipb = nullptr;
+  int32_t* sub_done = nullptr;
   uint64_t* seg = nullptr;       // sparse index: [Q][tiles/8][TT][8] segment of each (query,
                                  // term position, tile) (start | len << 32), built per search
   int64_t cap_seg = 0;           // u64 entries of seg

@@ -128,6 +128,7 @@ struct Stage {
                              // main stage's queries left to the block merge)
   bool unsorted;             // merge_fast: a doc shard's list for the W-way merge — its
                              // keys >= the k-th, in no order (padding last): no sort
+  bool split;                // REST: over split items (ws.sub, built by bound_keys_kernel)
 };
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -1009,8 +1010,8 @@ __device__ __forceinline__ uint32_t scan64(uint32_t x) {
   return x;
 }
 
-struct FlatCur {    // XCD-relative item ordinal, its claim's end, band, stage query, batch row, band width
-  int32_t rit, end, b, q, qb, bw;
+struct FlatCur {    // XCD-relative item ordinal, its claim's end, first phase tile, stage
+  int32_t rit, end, b, q, qb, bw;  // query, batch row, tiles
 };
 
 struct FlatDesc {   // lane tile * 2^TL + term: the term's segment in the tile (raw; r1 == r0: none)
@@ -1106,8 +1107,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     uint64_t* __restrict__ list, int32_t* __restrict__ list_cnt, int32_t C,
     int32_t* __restrict__ wctr, int32_t claim_ch, int32_t claim_m,
     const uint64_t* __restrict__ skeys, int64_t sstride, int32_t BW, uint64_t* mirror,
-    int32_t* __restrict__ stats, int32_t* __restrict__ slot_cnt) {
+    int32_t* __restrict__ stats, int32_t* __restrict__ slot_cnt,
+    const uint32_t* __restrict__ sub, const int32_t* __restrict__ sub_ipb) {
   constexpr int D = 1 << S;
+  // REST over split items (SM == kSplitM): the per-search table `sub` gives
+  // each of a band's *sub_ipb items its query, first tile and width — a heavy
+  // query's band in 2..8 sub-items (bound_keys_kernel builds it), so the last
+  // items a wave claims are short and the waves end together
+  constexpr bool kSplit = PH == kRest && SM == kSplitM;
   constexpr int kFR = PH == kSample ? BM25_FR_S : BM25_FR;  // ring slots (>= 2)
   constexpr uint32_t TT = 1u << TL;                          // term lanes per tile
   constexpr uint32_t kTileMask = (64u >> TL) - 1u;           // tile of a segment lane
@@ -1124,7 +1131,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   const int32_t nq = (PH == kAll && nq_dev) ? uniform(*nq_dev) : nq_host;
   const int32_t nt = PH == kSample ? (int32_t)sample_count(a.ntiles, P, G) : (int32_t)a.ntiles;
   const int32_t nb = (nt + BW - 1) / BW;  // items: (query, BW consecutive phase tiles)
-  const int64_t nitems = (int64_t)nb * nq;
+  const int32_t ipb = kSplit ? uniform(*sub_ipb) : nq;  // items per band
+  const int64_t nitems = (int64_t)nb * ipb;
   const int64_t per = (nitems + 7) >> 3;
   const int grp = (int)(blockIdx.x & 7);
   const uint32_t lo = (uint32_t)(grp * per);
@@ -1157,6 +1165,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   const uint32_t lt = lane & (TT - 1u), li = lane >> TL;  // segment lane: tile li, term lt
   const int64_t nbp = (a.ntiles + 7) >> 3;                // 8-tile groups of the sparse seg rows
 
+  // split items: ordinal -> (band, table entry: query | first tile << 20 |
+  // tiles << 26)
+  auto dec = [&](FlatCur& c, uint32_t it) {
+    const uint32_t band = it / (uint32_t)ipb;
+    const uint32_t e = uniform((int)sub[it - band * (uint32_t)ipb]);
+    c.q = (int32_t)(e & 0xFFFFFu);
+    c.qb = c.q;
+    c.b = (int32_t)(band * (uint32_t)BW + ((e >> 20) & 63u));
+    c.bw = min((int32_t)(e >> 26), nt - c.b);
+  };
   // ---- items: claims, terms -> segment descriptors
   auto claim = [&]() -> int32_t {
     int32_t v = 0;
@@ -1172,10 +1190,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     if (c.rit >= ngi) return c;
     if (c.rit + 1 < c.end) {
       ++c.rit;
+      if constexpr (kSplit) {
+        dec(c, lo + (uint32_t)c.rit);
+        return c;
+      }
       if (++c.q == nq) {
         c.q = 0;
-        ++c.b;
-        c.bw = min(BW, nt - c.b * BW);
+        c.b += BW;
+        c.bw = min(BW, nt - c.b);
       }
       c.qb = batch_row(c.q);
       return c;
@@ -1190,10 +1212,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     n.rit = (int32_t)bb;
     n.end = (int32_t)min<int64_t>(ngi, bb + claim_ch);
     const uint32_t it = lo + (uint32_t)bb;
-    n.b = (int32_t)(it / (uint32_t)nq);
-    n.q = (int32_t)(it - (uint32_t)n.b * (uint32_t)nq);
+    if constexpr (kSplit) {
+      dec(n, it);
+      return n;
+    }
+    const uint32_t band = it / (uint32_t)nq;
+    n.q = (int32_t)(it - band * (uint32_t)nq);
     n.qb = batch_row(n.q);
-    n.bw = min(BW, nt - n.b * BW);
+    n.b = (int32_t)band * BW;
+    n.bw = min(BW, nt - n.b);
     return n;
   };
   auto terms_of = [&](const FlatCur& c) -> int32_t {
@@ -1211,7 +1238,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     const int32_t term = tm;
     const bool ok = (int)lt < T && (int)li < c.bw && term >= 0 && term < a.V;
     const int64_t tt = ok ? term : 0;
-    const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b * BW + li), (uint32_t)P,
+    const int64_t tile = ok ? (int64_t)tile_of32<PH>((uint32_t)(c.b + li), (uint32_t)P,
                                                       (uint32_t)G)
                             : 0;
     if constexpr (SP) {  // outside the item: the zero entry past the table
@@ -1264,7 +1291,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
     ++tr_items;
 #endif
     const bool th_pos = PH == kRest && th_positive(thN);
-    const uint32_t t32 = (uint32_t)(nx.b * BW) + li;  // REST: phase tile = tile
+    const uint32_t t32 = (uint32_t)nx.b + li;  // REST: phase tile = tile
     const bool smp = skipping && ((t32 >> lgG) & (uint32_t)(P - 1)) == 0u;
     bool skip = smp && th_pos && dN.aux < (uint32_t)(thN >> 32);
     if constexpr (PH == kRest) {
@@ -1299,7 +1326,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
       // its keys are written here (0: no positive sum)
       const uint32_t tr = seg_sum_u32<TL>(nr);
       if (lt == 0u && (int)li < nx.bw && tr == 0u) {
-        uint64_t* out = cand + (int64_t)nx.q * cstride + (int64_t)(nx.b * BW + (int32_t)li) * SM;
+        uint64_t* out = cand + (int64_t)nx.q * cstride + (int64_t)(nx.b + (int32_t)li) * SM;
 #pragma unroll
         for (int i = 0; i < SM; ++i) out[i] = 0ull;
         if (SM == 1 && mirror) mirror[out - cand] = 0ull;
@@ -1428,7 +1455,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BM25_FLAT_WP
   int32_t ncross = 0;
 
   auto epilogue = [&]() {
-    const int32_t ti = ctxE.b * BW + (int32_t)curTi;
+    const int32_t ti = ctxE.b + (int32_t)curTi;
     const int64_t tile = tile_of32<PH>((uint32_t)ti, (uint32_t)P, (uint32_t)G);
     if constexpr (kCross) {  // the large-k list path: per-tile slots
       const int64_t si = (int64_t)ctxE.q * a.ntiles + tile;
@@ -1856,6 +1883,78 @@ __device__ __forceinline__ void block_kth_u16(const uint64_t* lbq, int32_t nq4, 
   need = nd;
 }
 
+// The REST pass's split-item table (score_flat_kernel, SM == kSplitM), built
+// by the threshold blocks of one search: each block stores its query's weight
+// (the postings of its distinct terms in this index); the last block to
+// finish (a device-scope counter, reset for the next search) splits each
+// query's band into f(q) sub-items of bwmax / f(q) tiles — f(q) the power of
+// two >= weight / (1.25 x the batch's mean weight), at most bwmax — and lays
+// them out in query order: entry = q | first tile << 20 | tiles << 26, and
+// *sub_ipb = the items per band.  The heavy queries' items shrink to about
+// the mean, so the last items the waves claim end close together.
+__device__ void split_table(const IndexArgs& a, const int32_t* __restrict__ queries, int32_t T,
+                            int64_t q, int32_t nq, int32_t bwmax, uint32_t* __restrict__ qw,
+                            uint32_t* __restrict__ sub, int32_t* __restrict__ sub_ipb,
+                            int32_t* __restrict__ sub_done, uint32_t* sh /* >= 2 + kBoundNT / 64 */) {
+  __shared__ int32_t s_last;
+  if (threadIdx.x == 0) {
+    const int32_t* qt = queries + q * T;
+    uint64_t w = 0;
+    for (int i = 0; i < T; ++i) {
+      const int32_t t = qt[i];
+      bool dup = t < 0 || (int64_t)t >= a.V;
+      for (int j = 0; j < i && !dup; ++j) dup = qt[j] == t;
+      if (!dup) w += (uint64_t)(a.indptr[t + 1] - a.indptr[t]);
+    }
+    qw[q] = (uint32_t)min<uint64_t>(w, 0xFFFFFFFFull);
+    __threadfence();
+    s_last = atomicAdd(sub_done, 1) == nq - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // every block's weight is visible past the counter
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  // the batch's mean weight
+  uint64_t tw = 0;
+  for (int32_t i = (int32_t)threadIdx.x; i < nq; i += kBoundNT) tw += __hip_atomic_load(qw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t tw32 = (uint32_t)min<uint64_t>(tw, 0xFFFFFFFFull);
+  tw32 = wave_sum_u32(tw32);  // (a u32 sum of the batch: saturates only past 4 G postings)
+  if (lane == 0) sh[2 + wv] = tw32;
+  __syncthreads();
+  uint64_t tot = 0;
+#pragma unroll
+  for (int i = 0; i < kBoundNT / 64; ++i) tot += sh[2 + i];
+  const double lim = 1.25 * (double)tot / (double)nq;  // f = 1 up to 1.25 x the mean
+  // f(q) per query (thread t: queries t * per .. ), then a block scan of the counts
+  const int32_t per = (nq + kBoundNT - 1) / kBoundNT;
+  const int32_t q0 = (int32_t)threadIdx.x * per;
+  uint32_t fsum = 0u;
+  for (int32_t i = q0; i < min(nq, q0 + per); ++i) {
+    const double w = (double)__hip_atomic_load(qw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t f = 1u;
+    while ((int32_t)f < bwmax && w > lim * (double)f) f <<= 1;
+    fsum += f;
+  }
+  const uint32_t incl = wave_incl_scan(fsum);
+  __syncthreads();  // (sh[2..] reused)
+  if (lane == 63) sh[2 + wv] = incl;
+  __syncthreads();
+  uint32_t base = incl - fsum;
+  for (int i = 0; i < (int)wv; ++i) base += sh[2 + i];
+  for (int32_t i = q0; i < min(nq, q0 + per); ++i) {
+    const double w = (double)__hip_atomic_load(qw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t f = 1u;
+    while ((int32_t)f < bwmax && w > lim * (double)f) f <<= 1;
+    const uint32_t width = (uint32_t)bwmax / f;
+    for (uint32_t j = 0; j < f; ++j) sub[base + j] = (uint32_t)i | ((j * width) << 20) | (width << 26);
+    base += f;
+  }
+  if (threadIdx.x == kBoundNT - 1) {
+    *sub_ipb = (int32_t)base;  // (the last thread's end: every query's count)
+    *sub_done = 0;
+  }
+}
+
 __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
                                                               const uint16_t* __restrict__ bmax,
                                                               const int32_t* __restrict__ queries,
@@ -1864,7 +1963,12 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
                                                               uint64_t* __restrict__ theta,
                                                               int32_t* __restrict__ list_cnt,
                                                               int32_t* __restrict__ counters,
-                                                              int32_t nranks, int64_t wstride) {
+                                                              int32_t nranks, int64_t wstride,
+                                                              uint32_t* __restrict__ qw,
+                                                              uint32_t* __restrict__ sub,
+                                                              int32_t* __restrict__ sub_ipb,
+                                                              int32_t* __restrict__ sub_done,
+                                                              int32_t nq, int32_t bwmax) {
   extern __shared__ uint64_t lbq[];  // lb_j as u16, four tiles per u64 (zero past the last)
   const int64_t q = blockIdx.x;
   // world bounds (nranks > 0, theta mode): the rows of every shard, [nranks][V]
@@ -1926,6 +2030,7 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
       }
       list_cnt[q] = 0;
     }
+    if (sub != nullptr) split_table(a, queries, T, q, nq, bwmax, qw, sub, sub_ipb, sub_done, hist);
     return;
   }
   // the S-th largest lb and how many of the tiles at it are kept
@@ -3403,7 +3508,9 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
     // every claim counter of an XCD range needs a wave: counter cm is served
     // by the workgroups with (blockIdx / 8) % claim_m == cm
     const int claim_m = std::max(1, std::min(ix.opt.claim_m, grid / 8));
-    const int bw = flat_band(ix.opt, nt, sg.nq_host, grid, 64 >> TL, sg.nq_dev != nullptr);
+    // (split items: the table was built for bands of 64 >> TL tiles)
+    const int bw = SM == kSplitM ? (64 >> TL)
+                                 : flat_band(ix.opt, nt, sg.nq_host, grid, 64 >> TL, sg.nq_dev != nullptr);
     ix.disp.kernels |= PH == kSample ? kKFlatSample : (PH == kRest ? kKFlatRest : kKFlatAll);
     if (PH == kRest && SM == 2) ix.disp.kernels |= kKCountSkips;
     ix.disp.term_lanes = 1 << TL;
@@ -3414,7 +3521,8 @@ static void launch_flat(const DevIndex& ix, const int32_t* q, int64_t T, int64_t
                        ws.list, ws.list_cnt, ws.list_cap, wctr, ix.opt.claim_ch, claim_m,
                        skip ? sg.sample_keys : nullptr, sg.sample_stride, bw,
                        PH == kSample && SM == 1 ? sg.cand_mirror : nullptr,
-                       PH == kRest ? ws.counters + 5 : nullptr, kSlots ? ws.slot_cnt : nullptr);
+                       PH == kRest ? ws.counters + 5 : nullptr, kSlots ? ws.slot_cnt : nullptr,
+                       SM == kSplitM ? ws.sub : nullptr, SM == kSplitM ? ws.sub_ipb : nullptr);
   };
   if (ix.sparse)
     go(score_flat_kernel<S, PH, SM, true, TL>);
@@ -3449,6 +3557,8 @@ static void launch_phase(const DevIndex& ix, const int32_t* q, int64_t T, int64_
         return launch_flat_tl<S, PH, kLargeM>(ix, q, T, Qb, sg, ws, st);
       if (ix.opt.count_skips)  // the build that counts the skipped postings
         return launch_flat_tl<S, PH, 2>(ix, q, T, Qb, sg, ws, st);
+      if (sg.split && ws.sub != nullptr && flat_tl(T) == 3)  // split items (8-tile bands)
+        return launch_flat_tl<S, PH, kSplitM>(ix, q, T, Qb, sg, ws, st);
     }
     return launch_flat_tl<S, PH, 1>(ix, q, T, Qb, sg, ws, st);
   }
@@ -3592,8 +3702,10 @@ template <int S_>
 static void finish_s(const DevIndex& ix, const int32_t* q, int64_t Q, int64_t T, int k,
                      const SampleGeom& g, int W, const uint64_t* all_keys, const Workspace& ws,
                      hipStream_t st, bool theta_ready = false, hipStream_t st_rest = nullptr,
-                     hipEvent_t join = nullptr, hipEvent_t rest_timing = nullptr) {
+                     hipEvent_t join = nullptr, hipEvent_t rest_timing = nullptr,
+                     bool split = false) {
   Stage sg = main_stage(ix, Q, g.P, ws);
+  sg.split = split;
   // the score pass's stream: after everything enqueued on st so far
   auto to_rest = [&]() -> hipStream_t {
     if (st_rest == nullptr || st_rest == st || join == nullptr) {
@@ -3648,7 +3760,8 @@ hipError_t launch_sample(const DevIndex& ix, const int32_t* d_queries, int64_t Q
     hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT),
                        (size_t)(bmax_stride(ix.ntiles) * 2), stream, args_of(ix), ix.bmax,
                        d_queries, (int32_t)T, ix.tile_shift, g.S, keys, (uint64_t*)nullptr,
-                       (int32_t*)nullptr, (int32_t*)nullptr, 0, (int64_t)0);
+                       (int32_t*)nullptr, (int32_t*)nullptr, 0, (int64_t)0, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, 0, 0);
     return hipGetLastError();
   }
 #define CALL(s) sample_s<s>(ix, d_queries, Q, T, g, keys, ws, stream)
@@ -3727,6 +3840,16 @@ hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
   const SampleGeom g = shard_geom_world(ix, k, T, world);
   world = world && g.P == 0;
   const int64_t ntg = world ? ix.wtiles : ix.ntiles;
+  // split REST items where the waves get few items each (a doc shard of a
+  // few GPUs' collection: ~16 at W = 8): the heavy queries' last items set
+  // when the pass ends
+  static int cus = 0;
+  if (cus == 0 && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix.device) != hipSuccess)
+    cus = 256;
+  const bool split = ix.opt.rest_split && ws.sub != nullptr && g.P == 0 && flat_tl(T) == 3 &&
+                     use_flat(ix, T, Q) && Q < (1 << 20) &&
+                     ((ix.ntiles + 7) / 8) * Q < (int64_t)kSplitItemsPerWave * 19 * cus;
+  if (split) ix.disp.kernels |= kKRestSplit;
   if (g.P == 0 && Q > 0 && ix.ntiles > 0) {
     // one index: the bound kernel selects theta itself (no key list, no theta
     // kernel); world: the threshold of the whole collection, from every
@@ -3739,8 +3862,11 @@ hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
     hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT), lds, stream,
                        args_of(ix), world ? ix.wbmax : ix.bmax, d_queries, (int32_t)T,
                        ix.tile_shift, (int64_t)k, (uint64_t*)nullptr, ws.theta, ws.list_cnt,
-                       ws.counters, world ? ix.wW : 0, world ? ix.wstride : (int64_t)0);
-#define CALL(s) finish_s<s>(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream, true)
+                       ws.counters, world ? ix.wW : 0, world ? ix.wstride : (int64_t)0, ws.qw,
+                       split ? ws.sub : (uint32_t*)nullptr, ws.sub_ipb, ws.sub_done, (int32_t)Q,
+                       64 >> flat_tl(T));
+#define CALL(s) finish_s<s>(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream, true, nullptr, \
+                            nullptr, nullptr, split)
     BM25_SHIFT_DISPATCH(CALL)
 #undef CALL
     return hipGetLastError();

@@ -469,7 +469,8 @@ def main():
                     torch.cuda.synchronize()
                     ms = (time.perf_counter() - t0) * 1e3 / n
                     per_rank.append({"rank": r, "ms": round(ms, 4),
-                                     "fallback_queries": shards[r].search_stats()["fallback_queries"]})
+                                     "fallback_queries": shards[r].search_stats()["fallback_queries"],
+                                     "kernels": sorted(shards[r].last_dispatch()["kernels"])})
                 worst = max(x["ms"] for x in per_rank)
                 inline = inline or pipe > 1 or gated
                 coll_us = 0.0 if inline else (model_gather_us(list_b, W) if

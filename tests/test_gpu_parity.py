@@ -228,7 +228,7 @@ def test_wave_kernel_long_and_empty_queries(gpu, T):
         _check_dispatch(index, k, T=T, flat=False)
     index.set_option("sample_p", 1)  # the exact pass over every tile
     _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
-    assert index.last_dispatch()["kernels"] - {"bound_off"} == {"wave_all"}
+    assert index.last_dispatch()["kernels"] - {"bound_off", "rest_split"} == {"wave_all"}
     index.set_option("list_cap", 4)  # every query through the fallback stage
     index.set_option("sample_p", 8)
     _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
@@ -268,7 +268,7 @@ def test_rescore_path_clustered_tile(gpu):
             got = index.search(q, k)
             _exact(got, oracle.search_c(N, ip, ix, dt, q, k))
             assert index.profile_read()["rescored_tiles_last"] > 0
-            assert (index.last_dispatch()["kernels"] - {"bound_off"}
+            assert (index.last_dispatch()["kernels"] - {"bound_off", "rest_split"}
                     == {"flat_all" if flat else "wave_all"})
 
 
@@ -452,7 +452,7 @@ def _check_dispatch(index, k, W=1, ntiles=None, opts=None, T=8, flat=True):
     weak = "bound_off" in d["kernels"]
     P = _geom_p(index, k, W, ntiles, opts, T=T, weak=weak)
     want = _want_kernels(P, flat)
-    assert d["kernels"] - {"bound_off"} == want and d["sample_p"] == P, (k, d, want, P)
+    assert d["kernels"] - {"bound_off", "rest_split"} == want and d["sample_p"] == P, (k, d, want, P)
     return d
 
 
@@ -1123,7 +1123,7 @@ def test_config4_c3_index_eight_shards_full_batch(gpu):
     dq = torch.from_numpy(q).cuda()
     _exact(_protocol_search(shards, dq, cfg.k, sdm), ref)
     d = shards[0].last_dispatch()
-    assert d["kernels"] - {"bound_off"} == _want_kernels(
+    assert d["kernels"] - {"bound_off", "rest_split"} == _want_kernels(
         _geom_p(shards[0], cfg.k, W, (sdm + 2047) // 2048, weak="bound_off" in d["kernels"])), d
     _progress("c4: two-collective protocol bit-exact")
     _exact(_world_bounds_search(shards, dq, cfg.k), ref)
@@ -1188,7 +1188,15 @@ def test_world_bounds_shards_ties_small_shards(gpu):
     with pytest.raises(ValueError, match="world bounds"):
         shards[0].search_shard_device(dq, 10, d, d.view(torch.float32))
     for k in (1, 10, 16, 5000):
-        _exact(_world_bounds_search(shards, dq, k), oracle.search_c(N, ip, ix, dt, q, k, threads=8))
+        ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
+        _exact(_world_bounds_search(shards, dq, k), ref)
+        if k <= 16:  # REST over split items (rest_split: heavy queries' bands in pieces)
+            for s in shards:
+                s.set_option("rest_split", 1)
+            _exact(_world_bounds_search(shards, dq, k), ref)
+            assert "rest_split" in shards[1].last_dispatch()["kernels"]
+            for s in shards:
+                s.set_option("rest_split", 0)
     for s in shards:
         s.close()
 
