@@ -413,7 +413,13 @@ int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
  *                    (per tile, its largest query-term maximum is a real
  *                    document's score lower bound) with no SAMPLE pass;
  *                    0: the sampled threshold.  Every shard of a multi-rank
- *                    search needs the same setting (bm25_sample_width)
+ *                    search needs the same setting (bm25_sample_width).  A
+ *                    handle whose tile-bound searches overflowed switches
+ *                    itself to the sampled threshold for a while, decided per
+ *                    handle from a host-mapped report read without waiting —
+ *                    so ranks may mix the two kinds of keys in one search:
+ *                    that is exact (both are keys of real documents, the
+ *                    width S is the same), only the work differs
  *   "large_lists"    1 (default): k > 4096 takes the list path where it
  *                    applies (a sampled threshold, keys above it listed by the
  *                    REST pass, selected and sorted — no dense score rows);
