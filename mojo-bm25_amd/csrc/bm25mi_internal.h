@@ -71,7 +71,7 @@ constexpr int kWctrRegions = 3;
 struct SearchOpts {
   int flat = 1;            // 0: score_wave_kernel for every phase
   int flat_bw = 0;         // tiles per flat item: 0 = auto, else 1, 2, 4 or 8
-  int items_per_wave = 8;  // auto flat_bw: halve while a phase gives fewer items per wave
+  int items_per_wave = 4;  // auto flat_bw: halve while a phase gives fewer items per wave (c2: 4 > 8)
   int sample_p = 8;        // largest sampling stride (1: the exact pass over every tile)
   int list_cap = 0;        // candidate-list capacity per query (0: auto)
   int claim_ch = 1;        // flat items per claim
