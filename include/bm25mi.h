@@ -297,7 +297,11 @@ int bm25_search_finish_streams_device(bm25_index* idx, const int32_t* d_queries,
  *     rounded up to 4; the same on every rank; zero past its tiles);
  *   (caller) all-gather -> d_world [world][n_terms][stride], kept alive;
  *   bm25_index_set_world_bounds(idx, d_world, world, stride, world_tiles):
- *     world_tiles = the collection's tiles (NULL d_world clears);
+ *     world_tiles = the collection's tiles (NULL d_world clears); d_world
+ *     must be complete when called: the handle reads it once on its own
+ *     stream into a pooled copy it owns (the max of every 4 tiles, a quarter
+ *     of the size: the threshold's input where the collection has >= 8k such
+ *     groups — option bound_pool) and keeps the pointer for the rest;
  *   bm25_search_shard_device(...): this shard's keys >= the collection's
  *     threshold (k real documents score at least it) as a [Q, k] list in no
  *     particular order (global doc ids, padding doc -1 / score bits
@@ -389,7 +393,8 @@ int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
  * Search options of one handle.  A new handle takes them from the
  * environment (BM25_FLAT, BM25_FLAT_BW, BM25_ITEMS_PER_WAVE, BM25_SAMPLE_P,
  * BM25_LIST_CAP, BM25_CLAIM_CH, BM25_CLAIM_M, BM25_TILE_BOUND, BM25_THETA_BOUND,
- * BM25_GRID_PCT, BM25_LARGE_LISTS, BM25_COUNT_SKIPS) at
+ * BM25_GRID_PCT, BM25_LARGE_LISTS, BM25_COUNT_SKIPS, BM25_REST_SPLIT,
+ * BM25_BOUND_POOL) at
  * bm25_index_create; these
  * calls change or read them afterwards, effective from the next search.
  * Results never depend on them (every setting is bit-exact); they choose
@@ -435,6 +440,12 @@ int bm25_search_counters(bm25_index* idx, int64_t* out, int32_t n);
  *                    heavy query's 8-tile band is split into 2..8 items (a
  *                    per-search table built by the threshold kernel);
  *                    0 (default: measured no faster at W = 8)
+ *   "bound_pool"     1 (default): the tile-bound threshold reads the bounds
+ *                    pooled over groups of 4 tiles (a group's largest query-
+ *                    term maximum is still a lower bound of one of its
+ *                    documents' scores) where there are >= 8k groups — a
+ *                    quarter of the threshold kernel's bytes; 0: the per-tile
+ *                    bounds
  *   "grid_pct"       percent of the device's resident workgroup slots the
  *                    persistent score kernels launch (1..100, default 100):
  *                    below 100 leaves slots for kernels of another stream
@@ -456,7 +467,8 @@ int bm25_index_get_option(const bm25_index* idx, const char* name, int64_t* valu
  *                (more than 1/16 of their queries took the exact fallback) —
  *                it is retried after 64, 128, ... 4096 searches; 512 (a
  *                flag): REST counted its skipped postings (count_skips);
- *                1024 (a flag): REST ran over split items (rest_split)
+ *                1024 (a flag): REST ran over split items (rest_split);
+ *                2048 (a flag): the threshold read the pooled bounds (bound_pool)
  *   *term_lanes  flat kernel: term lanes per tile (8, 16, 32 or 64)
  *   band_tiles   [3]: flat kernel tiles per item of ALL, SAMPLE, REST
  *   *sample_p    sampling stride of the search (1: exact pass, 0: tile-bound

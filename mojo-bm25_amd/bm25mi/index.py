@@ -301,9 +301,10 @@ class GpuIndex:
 
     KERNELS = {1: "flat_sample", 2: "flat_rest", 4: "flat_all", 8: "wave_sample",
                16: "wave_rest", 32: "wave_all", 64: "large_k", 128: "bound_keys",
-               256: "bound_off", 512: "count_skips", 1024: "rest_split"}  # (flags, not
+               256: "bound_off", 512: "count_skips", 1024: "rest_split",
+               2048: "bound_pool"}  # (flags, not
     # kernels: 256 the tile-bound threshold was off, 512 REST counted the postings it
-    # skipped, 1024 REST ran over split items)
+    # skipped, 1024 REST ran over split items, 2048 the threshold read the pooled bounds)
 
     def last_dispatch(self) -> dict:
         """What the last search launched (bm25_search_dispatch): the score

@@ -151,6 +151,7 @@ SearchOpts env_opts() {
   o.count_skips = env_int("BM25_COUNT_SKIPS", o.count_skips) != 0;
   o.large_lists = env_int("BM25_LARGE_LISTS", o.large_lists) != 0;
   o.rest_split = env_int("BM25_REST_SPLIT", o.rest_split) != 0;
+  o.bound_pool = env_int("BM25_BOUND_POOL", o.bound_pool) != 0;
   return o;
 }
 
@@ -192,6 +193,9 @@ int set_opt(SearchOpts& o, const char* name, int64_t v) {
   } else if (n == "rest_split") {
     if (v != 0 && v != 1) return fail(BM25_EINVAL, "rest_split must be 0 or 1");
     o.rest_split = (int)v;
+  } else if (n == "bound_pool") {
+    if (v != 0 && v != 1) return fail(BM25_EINVAL, "bound_pool must be 0 or 1");
+    o.bound_pool = (int)v;
   } else if (n == "count_skips") {
     if (v != 0 && v != 1) return fail(BM25_EINVAL, "count_skips must be 0 or 1");
     o.count_skips = (int)v;
@@ -220,6 +224,7 @@ int get_opt(const SearchOpts& o, const char* name, int64_t* v) {
   else if (n == "count_skips") *v = o.count_skips;
   else if (n == "large_lists") *v = o.large_lists;
   else if (n == "rest_split") *v = o.rest_split;
+  else if (n == "bound_pool") *v = o.bound_pool;
   else return fail(BM25_EINVAL, "unknown option '%s'", name);
   return BM25_OK;
 }
@@ -665,6 +670,17 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
     if (hipMalloc(&ix.bmax, sizeof(uint16_t) * n_terms * bmax_stride(ntiles)) == hipSuccess) {
       TRYC(launch_build_bmax(ix, h->stream), "build_bmax launch");
       h->device_bytes += (int64_t)(sizeof(uint16_t) * n_terms * bmax_stride(ntiles));
+      // the pooled copy of the threshold kernel (a quarter of the bytes; optional)
+      const int64_t ps = bmax_stride((ntiles + kPool - 1) / kPool);
+      if (hipMalloc(&ix.bpool, sizeof(uint16_t) * n_terms * ps) == hipSuccess) {
+        ix.pstride = ps;
+        TRYC(launch_pool_bounds(ix.bmax, n_terms, bmax_stride(ntiles), ix.bpool, ps, h->stream),
+             "pool_bounds launch");
+        h->device_bytes += (int64_t)(sizeof(uint16_t) * n_terms * ps);
+      } else {
+        (void)hipGetLastError();
+        ix.bpool = nullptr;
+      }
     } else {
       (void)hipGetLastError();
       ix.bmax = nullptr;
@@ -680,7 +696,8 @@ int bm25_index_create(int device, int64_t n_docs, int64_t n_terms, int64_t nnz,
                         "(canonical CSC)"));
   h->arrays = std::make_shared<IndexArrays>();
   h->arrays->device = device;
-  h->arrays->p = {ix.indptr, ix.rel, ix.tl_ptr, ix.tl_tile, ix.tl_start, ix.ldoc, ix.val, ix.bmax};
+  h->arrays->p = {ix.indptr, ix.rel, ix.tl_ptr, ix.tl_tile, ix.tl_start, ix.ldoc, ix.val, ix.bmax,
+                  ix.bpool};
   *out = h;
   return cleanup(BM25_OK);
 }
@@ -712,13 +729,16 @@ int bm25_index_destroy(bm25_index* h) {
   } else {              // a create that failed part-way
     for (void* x : {(void*)h->ix.indptr, (void*)h->ix.rel, (void*)h->ix.tl_ptr,
                     (void*)h->ix.tl_tile, (void*)h->ix.tl_start, (void*)h->ix.ldoc,
-                    (void*)h->ix.val, (void*)h->ix.bmax})
+                    (void*)h->ix.val, (void*)h->ix.bmax, (void*)h->ix.bpool})
       hipFree(x);
   }
+  hipFree(h->ix.wbpool);  // (the handle's own pooled world bounds)
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return BM25_OK;
 }
+
+static int pool_world(bm25_index* h);
 
 int bm25_index_fork(bm25_index* base, bm25_index** out) {
   if (!out) return fail(BM25_EINVAL, "out is NULL");
@@ -729,6 +749,7 @@ int bm25_index_fork(bm25_index* base, bm25_index** out) {
   bm25_index* h = new bm25_index();
   h->ix = base->ix;  // the same device arrays and options; its own dispatch report
   h->ix.disp = Dispatch{};
+  h->ix.wbpool = nullptr;  // (the base's own; the fork pools the world table itself, below)
   h->arrays = base->arrays;
   h->device_bytes = base->device_bytes;
   const hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -737,6 +758,13 @@ int bm25_index_fork(bm25_index* base, bm25_index** out) {
     return hip_fail(e, "hipStreamCreate");
   }
   alloc_report(h);
+  if (h->ix.wbmax) {
+    const int rc = pool_world(h);
+    if (rc) {
+      bm25_index_destroy(h);
+      return rc;
+    }
+  }
   *out = h;
   return BM25_OK;
 }
@@ -831,14 +859,46 @@ int bm25_index_bounds_export(bm25_index* h, uint16_t* d_out, int64_t stride, voi
   return BM25_OK;
 }
 
+// The pooled world table (DevIndex::wbpool) of a handle with world bounds,
+// built on the handle's stream from the caller's finished table and owned by
+// the handle; without the memory, none (the per-tile table serves).
+static int pool_world(bm25_index* h) {
+  DevIndex& ix = h->ix;
+  const int64_t ps = bmax_stride(ix.wstride / kPool);
+  const int64_t rows = (int64_t)ix.wW * ix.n_terms;
+  if (rows > 0 && hipMalloc(&ix.wbpool, sizeof(uint16_t) * rows * ps) == hipSuccess) {
+    HIP_TRY(launch_pool_bounds(ix.wbmax, rows, ix.wstride, ix.wbpool, ps, h->stream), "pool_bounds launch");
+    HIP_TRY(hipStreamSynchronize(h->stream), "pool_bounds");
+    ix.wpstride = ps;
+    // (a lower estimate of the collection's groups: each shard has ceil(its
+    // tiles / kPool) of them)
+    ix.wgroups = std::min<int64_t>((ix.wtiles + kPool - 1) / kPool, (int64_t)ix.wW * ps);
+  } else {
+    (void)hipGetLastError();
+    ix.wbpool = nullptr;
+    ix.wpstride = ix.wgroups = 0;
+  }
+  return BM25_OK;
+}
+
 int bm25_index_set_world_bounds(bm25_index* h, const uint16_t* d_world, int32_t world,
                                 int64_t stride, int64_t world_tiles) {
   if (!h) return fail(BM25_EINVAL, "NULL index");
   std::lock_guard<std::mutex> lk(h->mu);
-  if (!d_world) {
+  auto clear = [&]() {
+    if (h->ix.wbpool) {  // (searches still reading it: on the handle's last stream)
+      if (h->ws_stream) hipStreamSynchronize(h->ws_stream);
+      hipStreamSynchronize(h->stream);
+      hipFree(h->ix.wbpool);
+    }
     h->ix.wbmax = nullptr;
+    h->ix.wbpool = nullptr;
     h->ix.wW = 0;
-    h->ix.wstride = h->ix.wtiles = 0;
+    h->ix.wstride = h->ix.wtiles = h->ix.wpstride = h->ix.wgroups = 0;
+  };
+  if (!d_world) {
+    HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+    clear();
     return BM25_OK;
   }
   if (!h->ix.bmax)
@@ -850,11 +910,13 @@ int bm25_index_set_world_bounds(bm25_index* h, const uint16_t* d_world, int32_t 
   if ((int64_t)world * stride > kBoundMaxTiles + 4 * (int64_t)world)
     return fail(BM25_EINVAL, "world bounds of %lld tiles exceed the %lld one block selects over",
                 (long long)((int64_t)world * stride), (long long)kBoundMaxTiles);
+  HIP_TRY(hipSetDevice(h->ix.device), "hipSetDevice");
+  clear();
   h->ix.wbmax = d_world;
   h->ix.wW = world;
   h->ix.wstride = stride;
   h->ix.wtiles = world_tiles;
-  return BM25_OK;
+  return pool_world(h);
 }
 
 int bm25_search_shard_device(bm25_index* h, const int32_t* d_queries, int64_t Q, int64_t T,

@@ -83,6 +83,8 @@ struct SearchOpts {
   int grid_pct = 100;      // percent of the resident slots the persistent score kernels take
   int large_lists = 1;     // k > kMaxK: the list path (0: dense score rows for every query)
   int rest_split = 0;      // REST over split items where the waves get few items (measured: no gain)
+  int bound_pool = 1;      // the tile-bound threshold from the pooled bounds (bpool / wbpool) where
+                           // they hold >= kPoolGroupsPerK * k groups
 };
 
 // What the last search launched (bm25_search_dispatch).
@@ -95,6 +97,7 @@ enum {
                      // earlier ones overflowed with it (DevIndex::bound_weak)
   kKCountSkips = 512,  // (a flag) REST counted the postings its tile bound skipped
   kKRestSplit = 1024,  // (a flag) REST ran over split items (heavy queries' bands in pieces)
+  kKBoundPool = 2048,  // (a flag) the tile-bound threshold came from the pooled bounds
 };
 struct Dispatch {
   uint32_t kernels = 0;       // kK* bits of the score kernels launched
@@ -133,6 +136,13 @@ struct DevIndex {
   // bound of that score (threshold keys) and, one f16 step up, an upper bound
   // (the REST pass's tile skip)
   uint16_t* bmax = nullptr;
+  // The same bounds pooled over groups of kPool consecutive tiles (the max of
+  // each group's entries, [V][pstride], pstride = bmax_stride(ceil(ntiles /
+  // kPool))): the threshold kernel's input where it holds enough groups — a
+  // group's bound is still <= one of its documents' scores, and distinct
+  // groups hold distinct documents, at a quarter of the bytes
+  uint16_t* bpool = nullptr;
+  int64_t pstride = 0;
   // The tile-bound threshold is off for this handle's next searches: the
   // last ones that used it overflowed their candidate lists (weak bounds —
   // an index whose terms weigh alike); set by the host per search
@@ -147,6 +157,12 @@ struct DevIndex {
   int32_t wW = 0;
   int64_t wstride = 0;
   int64_t wtiles = 0;
+  // ... and pooled as bpool (handle-owned, built by bm25_index_set_world_bounds):
+  // [wW][V][wpstride], wpstride = bmax_stride(wstride / kPool); wgroups = the
+  // collection's groups (each shard's ceil(tiles / kPool), summed)
+  uint16_t* wbpool = nullptr;
+  int64_t wpstride = 0;
+  int64_t wgroups = 0;
   SearchOpts opt;
   mutable Dispatch disp;  // written by the launchers (callers hold the handle's mutex)
 };
@@ -236,6 +252,11 @@ SampleGeom search_geom(const DevIndex& ix, int64_t ntiles, int k, int W, int64_t
 constexpr int64_t kBoundMaxTiles = 30720;
 // ... and at least this many tiles per wanted key over the whole collection.
 constexpr int64_t kBoundTilesPerK = 16;
+// Pooled bounds: tiles per group, and the groups per wanted key the pooled
+// threshold needs (else the per-tile bounds: top-k tiles sharing a group
+// lower the threshold by about k^2 (kPool - 1) / (2 ntiles) ranks).
+constexpr int64_t kPool = 4;
+constexpr int64_t kPoolGroupsPerK = 8;
 // ... and queries of at most this many terms (search_geom; the bound kernel's
 // per-tile loads in flight).
 #ifndef BM25_BOUND_TERMS
@@ -248,6 +269,10 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices,
                                int32_t* d_err, hipStream_t stream);
 // Tile bounds ix.bmax from the dense segment table and the scores.
 hipError_t launch_build_bmax(const DevIndex& ix, hipStream_t stream);
+// out[r][g] = the max of in[r][kPool g .. kPool g + kPool - 1] (u16 f16 bits,
+// all >= 0) for rows r < rows, g < out_stride (zero past in_stride).
+hipError_t launch_pool_bounds(const uint16_t* in, int64_t rows, int64_t in_stride, uint16_t* out,
+                              int64_t out_stride, hipStream_t stream);
 // Sparse segment table: non-empty tiles per term -> d_cnt[V] (also writes
 // ldoc and validates, as launch_build_tables), then (after the caller's scan
 // into ix.tl_ptr) the tile lists.

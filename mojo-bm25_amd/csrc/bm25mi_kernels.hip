@@ -1808,6 +1808,23 @@ __global__ __launch_bounds__(256) void build_bmax_kernel(const int64_t* __restri
   }
 }
 
+// Pooled tile bounds (DevIndex::bpool / wbpool): each group of kPool
+// consecutive entries of a row -> its max (f16 bits of values >= 0 order as
+// integers); groups past the input row are 0.  Once per index / world table.
+__global__ __launch_bounds__(256) void pool_bounds_kernel(const uint16_t* __restrict__ in,
+                                                          int64_t rows, int64_t in_stride,
+                                                          uint16_t* __restrict__ out,
+                                                          int64_t out_stride) {
+  const int64_t n = rows * out_stride;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / out_stride, g = e - r * out_stride;
+    uint16_t m = 0;
+    for (int64_t j = g * kPool; j < min<int64_t>((g + 1) * kPool, in_stride); ++j)
+      m = max(m, in[r * in_stride + j]);
+    out[e] = m;
+  }
+}
+
 // Tile-bound threshold keys (search_geom's P = 0), one workgroup per query:
 // for every tile j, lb_j = the largest of its query terms' tile maxima (bmax,
 // rounded down).  A document of the tile that holds such a maximum scores at
@@ -1955,6 +1972,62 @@ __device__ void split_table(const IndexArgs& a, const int32_t* __restrict__ quer
   }
 }
 
+// lb of every tile group of a query into lbq: the packed u16 maxima of its
+// terms' bmax rows (v_pk_max_u16), GPI groups per thread per round with all
+// their TMAX x GPI row loads issued before any is used.
+typedef unsigned short bm25_us4 __attribute__((ext_vector_type(4)));
+template <int TMAX, int GPI>
+__device__ __forceinline__ void bound_rows(const IndexArgs& a, const uint16_t* __restrict__ bmax,
+                                           const int32_t* __restrict__ qt, int32_t T, int64_t bs,
+                                           int32_t gpr, int32_t nq4, int64_t rrank, bool world,
+                                           uint64_t* lbq) {
+  const uint64_t* row[TMAX];
+  bool has[TMAX];
+#pragma unroll
+  for (int i = 0; i < TMAX; ++i) {
+    const int32_t t = i < T ? __builtin_amdgcn_readfirstlane(qt[i]) : -1;
+    has[i] = t >= 0 && (int64_t)t < a.V;
+    row[i] = reinterpret_cast<const uint64_t*>(bmax + (has[i] ? (int64_t)t * bs : 0));
+  }
+  for (int32_t g0 = (int32_t)threadIdx.x; g0 < nq4; g0 += GPI * kBoundNT) {
+    int64_t o[GPI];
+#pragma unroll
+    for (int j = 0; j < GPI; ++j) {
+      const int32_t g = g0 + j * kBoundNT;
+      const int32_t w = world ? g / gpr : 0;
+      o[j] = g < nq4 ? (int64_t)w * rrank + (g - w * gpr) : -1;
+    }
+    // every load unconditional at a valid address (a term slot without a term
+    // reads row 0, a group past the last reads group 0) and masked after it:
+    // a guarded load compiles to a branch with a wait of its own — one memory
+    // round trip per load
+    uint64_t v[GPI][TMAX];
+#pragma unroll
+    for (int j = 0; j < GPI; ++j)
+#pragma unroll
+      for (int i = 0; i < TMAX; ++i) v[j][i] = row[i][o[j] >= 0 ? o[j] : 0];
+#pragma unroll
+    for (int j = 0; j < GPI; ++j)
+#pragma unroll
+      for (int i = 0; i < TMAX; ++i) v[j][i] = (has[i] && o[j] >= 0) ? v[j][i] : 0ull;
+#pragma unroll
+    for (int j = 0; j < GPI; ++j) {
+      bm25_us4 m = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < TMAX; ++i) {
+        bm25_us4 x;
+        __builtin_memcpy(&x, &v[j][i], 8);
+        m = __builtin_elementwise_max(m, x);
+      }
+      if (o[j] >= 0) {
+        uint64_t mm;
+        __builtin_memcpy(&mm, &m, 8);
+        lbq[g0 + j * kBoundNT] = mm;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
                                                               const uint16_t* __restrict__ bmax,
                                                               const int32_t* __restrict__ queries,
@@ -1974,38 +2047,20 @@ __global__ __launch_bounds__(kBoundNT) void bound_keys_kernel(IndexArgs a,
   // world bounds (nranks > 0, theta mode): the rows of every shard, [nranks][V]
   // [wstride] — the groups of shard w follow those of shard w - 1 (a shard's
   // zero padding holds no positive tile); otherwise this index's [V][bs]
+  // (theta mode: wstride > 0 without world = the pooled table's row stride —
+  // its groups take the tiles' place, launch_score)
   const bool world = nranks > 0;
-  const int64_t bs = world ? wstride : bmax_stride(a.ntiles);  // a row holds whole groups
-  const int32_t gpr = (int32_t)(bs >> 2);                        // u64 groups per row
-  const int32_t nq4 = world ? nranks * gpr : (int32_t)((a.ntiles + 3) >> 2);
+  const int64_t bs = wstride > 0 ? wstride : bmax_stride(a.ntiles);  // a row holds whole groups
+  const int32_t gpr = (int32_t)(bs >> 2);                              // u64 groups per row
+  const int32_t nq4 = world ? nranks * gpr : gpr;
   const int64_t rrank = world ? a.V * (bs >> 2) : 0;             // u64 between two shards' rows
   // the query's terms (T <= kBoundMaxTerms, launch_sample checks), loaded at uniform
   // addresses with every lane active; padding and ids >= V: none
   const int32_t* qt = queries + q * T;
-  const uint64_t* row[kBoundMaxTerms];
-  bool has[kBoundMaxTerms];
-#pragma unroll
-  for (int i = 0; i < (int)kBoundMaxTerms; ++i) {
-    const int32_t t = i < T ? __builtin_amdgcn_readfirstlane(qt[i]) : -1;
-    has[i] = t >= 0 && (int64_t)t < a.V;
-    row[i] = reinterpret_cast<const uint64_t*>(bmax + (has[i] ? (int64_t)t * bs : 0));
-  }
-  for (int32_t g = (int32_t)threadIdx.x; g < nq4; g += kBoundNT) {
-    const int32_t w = world ? g / gpr : 0;
-    const int64_t o = (int64_t)w * rrank + (g - w * gpr);
-    uint64_t v[kBoundMaxTerms];
-#pragma unroll
-    for (int i = 0; i < (int)kBoundMaxTerms; ++i) v[i] = has[i] ? row[i][o] : 0ull;
-    uint64_t m = 0ull;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      uint32_t x = 0u;
-#pragma unroll
-      for (int i = 0; i < (int)kBoundMaxTerms; ++i) x = max(x, (uint32_t)(v[i] >> (16 * u)) & 0xFFFFu);
-      m |= (uint64_t)x << (16 * u);
-    }
-    lbq[g] = m;
-  }
+  if (T <= 8)  // (the common width: four groups per round, 32 loads in flight)
+    bound_rows<8, 4>(a, bmax, qt, T, bs, gpr, nq4, rrank, world, lbq);
+  else
+    bound_rows<kBoundMaxTerms, 2>(a, bmax, qt, T, bs, gpr, nq4, rrank, world, lbq);
   __syncthreads();
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   if (theta != nullptr) {
@@ -2342,7 +2397,11 @@ __global__ __launch_bounds__(64 * kQW) void theta_wave_kernel(const uint64_t* __
       for (int j = 0; j < kThetaR; ++j) {  // (32-bit division: n <= 1024)
         const uint32_t i = (uint32_t)j * 64u + lane;
         const uint32_t w = i / (uint32_t)S;
-        key[j] = i < (uint32_t)n ? all_keys[((int64_t)w * Q + q) * S + (i - w * (uint32_t)S)] : 0ull;
+        // (unconditional load at a valid index, masked after: a guarded load
+        // is a branch with a memory wait of its own)
+        const uint32_t ic = i < (uint32_t)n ? i : 0u, wc = ic / (uint32_t)S;
+        const uint64_t x = all_keys[((int64_t)wc * Q + q) * S + (ic - wc * (uint32_t)S)];
+        key[j] = i < (uint32_t)n ? x : 0ull;
       }
       // fewer than k real keys: the k-th is a zero key (no threshold)
       uint32_t nz = 0u, om = 0u, nm = 0u;
@@ -2608,7 +2667,8 @@ __device__ __forceinline__ void regs_sort_write(const uint64_t* keys, uint32_t n
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const uint32_t i = (uint32_t)j * 64u + lane;
-    key[j] = i < n ? keys[i] : 0ull;
+    const uint64_t x = keys[i < n ? i : 0u];  // (unconditional read, masked)
+    key[j] = i < n ? x : 0ull;
   }
   wave_sort_regs<R>(key);
 #pragma unroll
@@ -2677,7 +2737,8 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const int i = j * 64 + (int)lane;
-    const uint64_t x = i < cnt ? lst[i] : 0ull;
+    const uint64_t y = lst[i < cnt ? i : 0];  // (unconditional load, masked: a guarded
+    const uint64_t x = i < cnt ? y : 0ull;    // load waits for memory on its own)
     key[j] = x >= th ? x : 0ull;  // (every list key is >= theta; key 0 = empty)
   }
   uint32_t n = 0;
@@ -2914,7 +2975,8 @@ __device__ bool long_merge_sampled(const Stage& sg, int32_t k, int64_t doc_offse
 #pragma unroll
   for (int j = 0; j < RS; ++j) {
     const int64_t i = (int64_t)(j * 64 + (int)lane) * s;
-    smp[j] = i < cnt ? lst[i] : 0ull;
+    const uint64_t y = lst[i < cnt ? i : 0];
+    smp[j] = i < cnt ? y : 0ull;
   }
   const int32_t want = min((2 * k + s - 1) / s, 64 * RS);
   uint32_t nk = 0;
@@ -2925,7 +2987,8 @@ __device__ bool long_merge_sampled(const Stage& sg, int32_t k, int64_t doc_offse
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * 64 + (int)lane;
-      x[u] = i < cnt ? lst[i] : 0ull;
+      const uint64_t y = lst[i < cnt ? i : 0];
+      x[u] = i < cnt ? y : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -2967,7 +3030,8 @@ __device__ bool long_merge_one(const Stage& sg, int32_t k, int64_t doc_offset, i
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int i = i0 + u * 64 + (int)lane;
-        x[u] = i < cnt ? (uint32_t)(lst[i] >> 32) : 0u;
+        const uint64_t y = lst[i < cnt ? i : 0];
+        x[u] = i < cnt ? (uint32_t)(y >> 32) : 0u;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -3021,7 +3085,8 @@ __device__ bool long_merge_one(const Stage& sg, int32_t k, int64_t doc_offset, i
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * 64 + (int)lane;
-      x[u] = i < cnt ? lst[i] : 0ull;
+      const uint64_t y = lst[i < cnt ? i : 0];
+      x[u] = i < cnt ? y : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -3135,7 +3200,8 @@ __device__ bool block_long_merge(const Stage& sg, int32_t k, int64_t doc_offset,
 #pragma unroll
   for (int i = 0; i < kLongPT; ++i) {
     const int e = i * kMergeNT + (int)threadIdx.x;
-    const uint64_t v = e < cnt ? lst[e] : 0ull;
+    const uint64_t y = lst[e < cnt ? e : 0];  // (unconditional load, masked)
+    const uint64_t v = e < cnt ? y : 0ull;
     x[i] = v >= th ? v : 0ull;
   }
   if (threadIdx.x < 64) {
@@ -3267,7 +3333,8 @@ __device__ __forceinline__ void lds_merge_one(uint64_t* kb, uint32_t cnt, int32_
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const uint32_t i = (uint32_t)j * 64u + lane;
-    key[j] = i < cnt ? kb[i] : 0ull;
+    const uint64_t y = kb[i < cnt ? i : 0u];
+    key[j] = i < cnt ? y : 0ull;
   }
   uint32_t kept = 0;
   const uint64_t kth = wave_kth_key<R>(key, k, kept);
@@ -3356,6 +3423,16 @@ hipError_t launch_build_tables(const DevIndex& ix, const int32_t* d_indices, int
   hipLaunchKernelGGL(build_tables_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                      ix.indptr, d_indices, ix.n_terms, ix.n_docs, ix.tile_shift, ix.ntiles,
                      ix.rel, ix.ldoc, d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_pool_bounds(const uint16_t* in, int64_t rows, int64_t in_stride, uint16_t* out,
+                              int64_t out_stride, hipStream_t stream) {
+  if (rows <= 0 || out_stride <= 0) return hipSuccess;
+  const int64_t n = rows * out_stride;
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(pool_bounds_kernel, dim3(blocks), dim3(256), 0, stream, in, rows, in_stride,
+                     out, out_stride);
   return hipGetLastError();
 }
 
@@ -3858,11 +3935,21 @@ hipError_t launch_score(const DevIndex& ix, const int32_t* d_queries, int64_t Q,
       return hipErrorInvalidValue;
     if (seg_entries(ix, Q, T) > 0) launch_seg_table(ix, d_queries, Q, T, ws, stream);
     ix.disp.kernels |= kKBound;
-    const size_t lds = world ? (size_t)(ix.wW * ix.wstride * 2) : (size_t)(bmax_stride(ix.ntiles) * 2);
+    // the pooled bounds where they hold enough groups (a quarter of the bytes;
+    // the threshold only needs k groups' bounds, DevIndex::bpool)
+    const bool pool =
+        ix.opt.bound_pool &&
+        (world ? ix.wbpool != nullptr && ix.wgroups >= kPoolGroupsPerK * (int64_t)k
+               : ix.bpool != nullptr && (ix.ntiles + kPool - 1) / kPool >= kPoolGroupsPerK * (int64_t)k);
+    if (pool) ix.disp.kernels |= kKBoundPool;
+    const uint16_t* tb = world ? (pool ? ix.wbpool : ix.wbmax) : (pool ? ix.bpool : ix.bmax);
+    const int64_t tstride = world ? (pool ? ix.wpstride : ix.wstride) : (pool ? ix.pstride : 0);
+    const size_t lds = world ? (size_t)(ix.wW * tstride * 2)
+                             : (size_t)((pool ? ix.pstride : bmax_stride(ix.ntiles)) * 2);
     hipLaunchKernelGGL(bound_keys_kernel, dim3((unsigned)Q), dim3(kBoundNT), lds, stream,
-                       args_of(ix), world ? ix.wbmax : ix.bmax, d_queries, (int32_t)T,
+                       args_of(ix), tb, d_queries, (int32_t)T,
                        ix.tile_shift, (int64_t)k, (uint64_t*)nullptr, ws.theta, ws.list_cnt,
-                       ws.counters, world ? ix.wW : 0, world ? ix.wstride : (int64_t)0, ws.qw,
+                       ws.counters, world ? ix.wW : 0, tstride, ws.qw,
                        split ? ws.sub : (uint32_t*)nullptr, ws.sub_ipb, ws.sub_done, (int32_t)Q,
                        64 >> flat_tl(T));
 #define CALL(s) finish_s<s>(ix, d_queries, Q, T, k, g, 1, ws.cand, ws, stream, true, nullptr, \

@@ -228,7 +228,7 @@ def test_wave_kernel_long_and_empty_queries(gpu, T):
         _check_dispatch(index, k, T=T, flat=False)
     index.set_option("sample_p", 1)  # the exact pass over every tile
     _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
-    assert index.last_dispatch()["kernels"] - {"bound_off", "rest_split"} == {"wave_all"}
+    assert index.last_dispatch()["kernels"] - {"bound_off", "rest_split", "bound_pool"} == {"wave_all"}
     index.set_option("list_cap", 4)  # every query through the fallback stage
     index.set_option("sample_p", 8)
     _exact(index.search(q, 30), oracle.search_c(N, ip, ix, dt, q, 30))
@@ -268,7 +268,7 @@ def test_rescore_path_clustered_tile(gpu):
             got = index.search(q, k)
             _exact(got, oracle.search_c(N, ip, ix, dt, q, k))
             assert index.profile_read()["rescored_tiles_last"] > 0
-            assert (index.last_dispatch()["kernels"] - {"bound_off", "rest_split"}
+            assert (index.last_dispatch()["kernels"] - {"bound_off", "rest_split", "bound_pool"}
                     == {"flat_all" if flat else "wave_all"})
 
 
@@ -396,7 +396,15 @@ def test_config3_full_batch_parity(gpu):
     q = synth.make_queries(cfg)
     index = _idx(ip, ix, dt, cfg.n_docs)
     docs, scores = index.search(q, cfg.k)
-    _exact((docs, scores), oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k, threads=16))
+    ref = oracle.search_c(cfg.n_docs, ip, ix, dt, q, cfg.k, threads=16)
+    _exact((docs, scores), ref)
+    # the threshold read the pooled bounds (1221 groups >= 8k); the per-tile
+    # bounds give the same bits
+    assert "bound_pool" in index.last_dispatch()["kernels"]
+    index.set_option("bound_pool", 0)
+    _exact(index.search(q, cfg.k), ref)
+    assert "bound_pool" not in index.last_dispatch()["kernels"]
+    index.set_option("bound_pool", 1)
     # whole batch: sorted, unique ids in range, ties ordered by id
     assert np.all(np.diff(scores, axis=1) <= 0)
     assert all(len(set(r)) == cfg.k for r in docs.tolist())
@@ -452,7 +460,7 @@ def _check_dispatch(index, k, W=1, ntiles=None, opts=None, T=8, flat=True):
     weak = "bound_off" in d["kernels"]
     P = _geom_p(index, k, W, ntiles, opts, T=T, weak=weak)
     want = _want_kernels(P, flat)
-    assert d["kernels"] - {"bound_off", "rest_split"} == want and d["sample_p"] == P, (k, d, want, P)
+    assert d["kernels"] - {"bound_off", "rest_split", "bound_pool"} == want and d["sample_p"] == P, (k, d, want, P)
     return d
 
 
@@ -1123,11 +1131,11 @@ def test_config4_c3_index_eight_shards_full_batch(gpu):
     dq = torch.from_numpy(q).cuda()
     _exact(_protocol_search(shards, dq, cfg.k, sdm), ref)
     d = shards[0].last_dispatch()
-    assert d["kernels"] - {"bound_off", "rest_split"} == _want_kernels(
+    assert d["kernels"] - {"bound_off", "rest_split", "bound_pool"} == _want_kernels(
         _geom_p(shards[0], cfg.k, W, (sdm + 2047) // 2048, weak="bound_off" in d["kernels"])), d
     _progress("c4: two-collective protocol bit-exact")
     _exact(_world_bounds_search(shards, dq, cfg.k), ref)
-    assert "bound_keys" in shards[0].last_dispatch()["kernels"]
+    assert {"bound_keys", "bound_pool"} <= shards[0].last_dispatch()["kernels"]
     _progress("c4: one-collective protocol (world tile bounds) bit-exact")
     for s in shards:
         s.close()
@@ -1190,6 +1198,15 @@ def test_world_bounds_shards_ties_small_shards(gpu):
     for k in (1, 10, 16, 5000):
         ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
         _exact(_world_bounds_search(shards, dq, k), ref)
+        # the pooled world bounds: 293 tiles, 74 groups of 4 serve k <= 9
+        assert ("bound_pool" in shards[1].last_dispatch()["kernels"]) == (k == 1), k
+        if k == 1:
+            for s in shards:
+                s.set_option("bound_pool", 0)
+            _exact(_world_bounds_search(shards, dq, k), ref)
+            assert "bound_pool" not in shards[1].last_dispatch()["kernels"]
+            for s in shards:
+                s.set_option("bound_pool", 1)
         if k <= 16:  # REST over split items (rest_split: heavy queries' bands in pieces)
             for s in shards:
                 s.set_option("rest_split", 1)
@@ -1329,7 +1346,8 @@ def test_theta_bound_exact(gpu, T, big):
     the REST tile skip — ties at the threshold (quarter-step values), rows
     with fewer positive tiles than k (zero-fill), padding, duplicates, scores
     past f16's range and below its subnormals, and T > 64 (the wave kernel's
-    REST)."""
+    REST); the threshold from the pooled bounds (bound_pool: 428 groups of 4
+    tiles serve k <= 53) and from the per-tile bounds."""
     N, V = 3_500_000, 300  # 1709 tiles: >= 16k at k = 100 (search_geom)
     ip, ix, dt = _bound_case(70 + T, N, V, 30, big)
     rng = np.random.default_rng(T)
@@ -1345,15 +1363,20 @@ def test_theta_bound_exact(gpu, T, big):
         ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
         for tb in (1, 0):
             for tl in (1, 0):
-                index.set_option("theta_bound", tb)
-                index.set_option("tile_bound", tl)
-                _exact(index.search(q, k), ref)
-                d = _check_dispatch(index, k, opts={"theta_bound": tb}, T=T, flat=T <= 64)
-                P = d["sample_p"]
-                assert (P == 0) == (bool(tb) and T <= 16 and "bound_off" not in d["kernels"]), \
-                    (P, tb, T, d)
+                for pool in (1, 0):
+                    index.set_option("theta_bound", tb)
+                    index.set_option("tile_bound", tl)
+                    index.set_option("bound_pool", pool)
+                    _exact(index.search(q, k), ref)
+                    d = _check_dispatch(index, k, opts={"theta_bound": tb}, T=T, flat=T <= 64)
+                    P = d["sample_p"]
+                    assert (P == 0) == (bool(tb) and T <= 16 and "bound_off" not in d["kernels"]), \
+                        (P, tb, T, d)
+                    assert ("bound_pool" in d["kernels"]) == (P == 0 and bool(pool) and
+                                                              428 >= 8 * k), (pool, k, d)
     index.set_option("theta_bound", 1)
     index.set_option("tile_bound", 1)
+    index.set_option("bound_pool", 1)
     index.close()
 
 
