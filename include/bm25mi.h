@@ -297,9 +297,9 @@ int bm25_search_finish_streams_device(bm25_index* idx, const int32_t* d_queries,
  *     rounded up to 4; the same on every rank; zero past its tiles);
  *   (caller) all-gather -> d_world [world][n_terms][stride], kept alive;
  *   bm25_index_set_world_bounds(idx, d_world, world, stride, world_tiles):
- *     world_tiles = the collection's tiles (NULL d_world clears); d_world
- *     must be complete when called: the handle reads it once on its own
- *     stream into a pooled copy it owns (the max of every 4 tiles, a quarter
+ *     world_tiles = the collection's tiles (NULL d_world clears); the call
+ *     waits for the device (d_world written on any stream before it is
+ *     complete) and reads the table once into a pooled copy the handle owns (the max of every 4 tiles, a quarter
  *     of the size: the threshold's input where the collection has >= 8k such
  *     groups — option bound_pool) and keeps the pointer for the rest;
  *   bm25_search_shard_device(...): this shard's keys >= the collection's

@@ -860,13 +860,17 @@ int bm25_index_bounds_export(bm25_index* h, uint16_t* d_out, int64_t stride, voi
 }
 
 // The pooled world table (DevIndex::wbpool) of a handle with world bounds,
-// built on the handle's stream from the caller's finished table and owned by
-// the handle; without the memory, none (the per-tile table serves).
+// built on the handle's stream once the device is idle (the caller's table
+// finished on whatever stream wrote it) and owned by the handle; without the
+// memory, none (the per-tile table serves).
 static int pool_world(bm25_index* h) {
   DevIndex& ix = h->ix;
   const int64_t ps = bmax_stride(ix.wstride / kPool);
   const int64_t rows = (int64_t)ix.wW * ix.n_terms;
   if (rows > 0 && hipMalloc(&ix.wbpool, sizeof(uint16_t) * rows * ps) == hipSuccess) {
+    // the caller's table may still be in flight on any of its streams (the
+    // exports, the all-gather): the whole device first — a setup call
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     HIP_TRY(launch_pool_bounds(ix.wbmax, rows, ix.wstride, ix.wbpool, ps, h->stream), "pool_bounds launch");
     HIP_TRY(hipStreamSynchronize(h->stream), "pool_bounds");
     ix.wpstride = ps;

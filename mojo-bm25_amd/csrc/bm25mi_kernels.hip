@@ -3365,32 +3365,44 @@ __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
   uint64_t* kb = buf[wave];
   const uint32_t lane = lane_id();
   // the lists' real keys (most slots are padding: the world holds ~2-3 k keys
-  // >= theta) compacted into the wave's LDS slice: rank by rank, columns of
-  // 64 (all loads of a rank in flight; no index division)
+  // >= theta) compacted into the wave's LDS slice: columns of 64 keys over
+  // the ranks' lists (rank-major), eight columns' loads in flight at a time
+  // (W = 8, k = 100: all sixteen columns in two rounds), each load
+  // unconditional at a valid address and masked after it — a guarded load is
+  // a branch with a memory wait of its own; no index division
   uint32_t cnt = 0u;
   const int nc = (k + 63) >> 6;
-  for (int w = 0; w < W; ++w) {
-    const int64_t o = (int64_t)w * rstride + q * k;
-    for (int c0 = 0; c0 < nc; c0 += 4) {
-      float sv[4];
-      int32_t dv[4];
+  const int ncol = W * nc;
+  int cw = 0, cc = 0;  // (rank, column) of the round's first column
+  for (int b0 = 0; b0 < ncol; b0 += 8) {
+    float sv[8];
+    int32_t dv[8];
+    int w = cw, c = cc;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = (c0 + u) * 64 + (int)lane;
-        const bool in = c0 + u < nc && j < k;
-        sv[u] = in ? in_scores[o + j] : 0.f;
-        dv[u] = in ? in_docs[o + j] : -1;
+    for (int u = 0; u < 8; ++u) {
+      const int j = c * 64 + (int)lane;
+      const bool in = b0 + u < ncol && j < k;
+      const int64_t off = in ? (int64_t)w * rstride + q * k + j : q * k;
+      const float sy = in_scores[off];
+      const int32_t dy = in_docs[off];
+      sv[u] = in ? sy : 0.f;
+      dv[u] = in ? dy : -1;
+      if (++c == nc) {
+        c = 0;
+        ++w;
       }
+    }
+    cw = w;
+    cc = c;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool nz = dv[u] >= 0;  // (padding: doc -1)
-        const uint64_t b = __ballot(nz);
-        if (nz)
-          kb[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                             __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
-              make_key(sv[u], (uint32_t)dv[u]);
-        cnt += (uint32_t)__popcll(b);
-      }
+    for (int u = 0; u < 8; ++u) {
+      const bool nz = dv[u] >= 0;  // (padding: doc -1)
+      const uint64_t b = __ballot(nz);
+      if (nz)
+        kb[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                           __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
+            make_key(sv[u], (uint32_t)dv[u]);
+      cnt += (uint32_t)__popcll(b);
     }
   }
   // <= 512 keys: sorted whole in registers, the first k written; more: the

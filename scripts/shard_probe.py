@@ -42,6 +42,7 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "mojo-bm25_amd"), REPO]
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 if os.environ.get("VLIB"):  # a variant build of libbm25mi (dev: scripts/build_variant.sh)
@@ -353,6 +354,13 @@ def main():
                         for r, ix_ in enumerate(shards):
                             ix_.search_shard_device(q, k, gw[r, 0], gw[r, 1].view(torch.float32), st)
                         torch.cuda.synchronize()
+                        # the lists' sizes: each shard's keys >= theta (capped at
+                        # k), and their sum per query (the W-way merge's input)
+                        nk = (gw[:, 0] >= 0).sum(dim=2).cpu().numpy()  # [W, Q]
+                        pct = lambda a: {"p50": int(np.percentile(a, 50)),
+                                         "p99": int(np.percentile(a, 99)), "max": int(a.max())}
+                        list_sizes = {"per_shard": pct(nk), "at_k": int((nk >= k).sum()),
+                                      "merged": pct(nk.sum(axis=0))}
 
                         def one(r):
                             ix_ = shards[r]
@@ -448,6 +456,10 @@ def main():
                                                 2 * Q * k, out_d, out_s, st)
                 ranks = (range(W) if not ranks_env else
                          [int(x) for x in ranks_env.split(",") if int(x) < W])
+                # PROBE_PASSES > 1: every rank timed that many times (rank order
+                # repeated), its fastest pass kept — the first rank timed right
+                # after the shards' build otherwise reads a few percent slow
+                ranks = list(ranks) * max(1, int(os.environ.get("PROBE_PASSES", "1")))
                 per_rank = []
                 for r in ranks:
                     if many is not None:  # the pipelined batches: n in one issue sequence
@@ -471,6 +483,11 @@ def main():
                     per_rank.append({"rank": r, "ms": round(ms, 4),
                                      "fallback_queries": shards[r].search_stats()["fallback_queries"],
                                      "kernels": sorted(shards[r].last_dispatch()["kernels"])})
+                best = {}
+                for x in per_rank:
+                    if x["rank"] not in best or x["ms"] < best[x["rank"]]["ms"]:
+                        best[x["rank"]] = x
+                per_rank = [best[r] for r in sorted(best)]
                 worst = max(x["ms"] for x in per_rank)
                 inline = inline or pipe > 1 or gated
                 coll_us = 0.0 if inline else (model_gather_us(list_b, W) if
@@ -502,6 +519,8 @@ def main():
                                                           * len(rows), 1)},
                         "projected_ms": round(proj, 4),
                         "projected_qps": round(Q * R / proj * 1e3, 1)}
+                if world_b and W > 1:
+                    line["list_sizes"] = list_sizes
                 if w1_ms is not None:
                     line["speedup_vs_W1"] = round(w1_ms / proj * R * Q / (Q * R), 3)
                 print(json.dumps(line), flush=True)

@@ -1218,6 +1218,55 @@ def test_world_bounds_shards_ties_small_shards(gpu):
         s.close()
 
 
+def test_world_bounds_set_while_export_in_flight(gpu):
+    """bm25_index_set_world_bounds reads the caller's table into its pooled
+    copy only once the device is idle: the table is first filled with the
+    largest f16 bound (65504: a threshold no document reaches), then each
+    shard's export is queued on a side stream behind a spin kernel and the
+    world bounds are set at once, with no wait by the caller — a copy taken
+    before the exports land would hold 65504 and zero-fill every row."""
+    import scipy.sparse as sp
+    import torch
+    N, V = 600_000, 200
+    ip, ix, dt = _bound_case(93, N, V, 20)
+    rng = np.random.default_rng(9)
+    q = np.concatenate([rng.integers(0, 20, size=(32, 3)),
+                        rng.integers(20, V, size=(32, 3))], axis=1).astype(np.int32)
+    cuts = [0, 2048 * 100, N]
+    m = sp.csc_matrix((dt, ix, ip), shape=(N, V))
+    shards = []
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        s_ = m[lo:hi].tocsc()
+        s_.sort_indices()
+        shards.append(_idx(s_.indptr.astype(np.int64), s_.indices.astype(np.int32),
+                           s_.data.astype(np.float32), hi - lo, doc_offset=lo, segments="dense"))
+    W, k = len(shards), 1
+    stride = max(s_.bounds_stride() for s_ in shards)
+    tiles = sum(int(s_.info()["n_tiles"]) for s_ in shards)
+    wb = torch.full((W, V, stride), 0x7BFF, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(200_000_000)  # (~0.1 s of spinning ahead of the exports)
+    for r, s_ in enumerate(shards):
+        s_.bounds_export(wb[r], stride, side)
+    for s_ in shards:
+        s_.set_world_bounds(wb, W, stride, tiles)
+    dq = torch.from_numpy(q).cuda()
+    g = torch.empty((W, 2, len(q), k), dtype=torch.int32, device="cuda")
+    for r, s_ in enumerate(shards):
+        s_.search_shard_device(dq, k, g[r, 0], g[r, 1].view(torch.float32))
+        assert "bound_pool" in s_.last_dispatch()["kernels"]
+    from bm25mi.index import merge_sorted_device
+    md = torch.empty((len(q), k), dtype=torch.int32, device="cuda")
+    ms = torch.empty((len(q), k), dtype=torch.float32, device="cuda")
+    merge_sorted_device(0, g, g[:, 1].view(torch.float32), W, len(q), k, 2 * len(q) * k, md, ms)
+    torch.cuda.synchronize()
+    _exact((md.cpu().numpy(), ms.cpu().numpy()), oracle.search_c(N, ip, ix, dt, q, k, threads=8))
+    for s_ in shards:
+        s_.close()
+
+
 @pytest.mark.parametrize("segments", ["dense", "sparse"])
 def test_config5_rank_shard_full_batch(gpu, segments):
     """Config 5 at its own per-rank workload: one rank's doc shard of the
