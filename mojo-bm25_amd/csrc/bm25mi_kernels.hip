@@ -2743,31 +2743,28 @@ __device__ __forceinline__ void fast_merge_one(const Stage& sg, int32_t k, int64
   }
   uint32_t n = 0;
   if (sg.unsorted) {
-    // a doc shard's list for the W-way merge: at most k keys go out as they
-    // are, padding after them
+    // a doc shard's list for the W-way merge, which sorts: its best k keys
+    // (all of them when there are at most k) go out in no particular order —
+    // the k-th key selected in registers, no sort — padding after them
+    const uint64_t kth = wave_kth_key<R>(key, k, n);  // (0: every key kept)
+    uint32_t base = 0u;
 #pragma unroll
-    for (int j = 0; j < R; ++j) n += key[j] != 0ull;
-    if (wave_sum_u32(n) <= (uint32_t)k) {
-      uint32_t base = 0u;
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const bool keep = key[j] != 0ull;
-        const uint64_t b = __ballot(keep);
-        if (keep) {
-          const uint32_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-          docs[q * k + i] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)key[j]) + doc_offset);
-          scores[q * k + i] = key_score((uint32_t)(key[j] >> 32));
-        }
-        base += (uint32_t)__popcll(b);
+    for (int j = 0; j < R; ++j) {
+      const bool keep = key[j] != 0ull && key[j] >= kth;
+      const uint64_t b = __ballot(keep);
+      if (keep) {
+        const uint32_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        docs[q * k + i] = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)key[j]) + doc_offset);
+        scores[q * k + i] = key_score((uint32_t)(key[j] >> 32));
       }
-      for (int i = (int)base + (int)lane; i < k; i += 64) {
-        docs[q * k + i] = -1;
-        scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
-      }
-      return;
+      base += (uint32_t)__popcll(b);
     }
-    n = 0;
+    for (int i = (int)base + (int)lane; i < k; i += 64) {
+      docs[q * k + i] = -1;
+      scores[q * k + i] = __uint_as_float(0xFFFFFFFFu);
+    }
+    return;
   }
   if (R == 8 && k <= 128) {  // (also at R = 16 the kernel spills)
     // a longer list: a provisional threshold t1 from a sample (the list's
@@ -3407,6 +3404,45 @@ __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
   }
   // <= 512 keys: sorted whole in registers, the first k written; more: the
   // k-th key selected first, the keys at or above it sorted
+  if (k <= 128 && cnt > 256u) {
+    // a long merge at k <= 128 (W = 8, k = 100: up to 800 keys): a provisional
+    // threshold t1 from 128 keys sampled at a stride over the list (sorted in
+    // registers: the sample key at the rank where ~1.5 k keys are expected at
+    // or above it); when k to 256 keys reach t1 — they hold the top k — those
+    // are compacted and sorted in registers, not the whole list
+    uint64_t smp[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) smp[j] = kb[(((uint32_t)j * 64u + lane) * cnt) >> 7];
+    wave_sort_regs<2>(smp);
+    const int r = min(127, max(0, (int)((3u * (uint32_t)k * 64u) / cnt)));
+    const uint64_t t1 = __shfl(r >= 64 ? smp[1] : smp[0], r & 63, 64);
+    uint64_t key[kMergeSortedCap / 64];
+    uint32_t c = 0u;
+#pragma unroll
+    for (int j = 0; j < kMergeSortedCap / 64; ++j) {
+      const uint32_t i = (uint32_t)j * 64u + lane;
+      const uint64_t y = kb[i < cnt ? i : 0u];
+      key[j] = i < cnt ? y : 0ull;
+      c += key[j] != 0ull && key[j] >= t1;
+    }
+    c = wave_sum_u32(c);
+    if (t1 != 0ull && c >= (uint32_t)k && c <= 256u) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      uint32_t base = 0u;
+#pragma unroll
+      for (int j = 0; j < kMergeSortedCap / 64; ++j) {
+        const bool keep = key[j] != 0ull && key[j] >= t1;
+        const uint64_t b = __ballot(keep);
+        if (keep)
+          kb[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = key[j];
+        base += (uint32_t)__popcll(b);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      regs_sort_write<4>(kb, base, k, 0, q, docs, scores);
+      return;
+    }
+  }
   if (cnt <= 512u) {
     sort_write_any<8>(kb, cnt, k, 0, q, docs, scores);
     return;
