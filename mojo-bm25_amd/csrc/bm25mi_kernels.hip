@@ -975,7 +975,10 @@ __global__ __launch_bounds__(64 * kWaves) void score_wave_kernel(
 // wavefronts per workgroup of the one-wave-per-query kernels (theta_wave,
 // merge_fast, merge_sorted); measured: one-wave workgroups change nothing
 // (profiles/r04/rejected/qw1_*)
-constexpr int kQW = 4;
+#ifndef BM25_QW
+#define BM25_QW 4
+#endif
+constexpr int kQW = BM25_QW;
 #ifndef BM25_FR    // rows in flight (ring slots): REST / ALL, SAMPLE
 #define BM25_FR 10
 #endif
@@ -3407,14 +3410,16 @@ __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
   if (k <= 128 && cnt > 256u) {
     // a long merge at k <= 128 (W = 8, k = 100: up to 800 keys): a provisional
     // threshold t1 from 128 keys sampled at a stride over the list (sorted in
-    // registers: the sample key at the rank where ~1.5 k keys are expected at
-    // or above it); when k to 256 keys reach t1 — they hold the top k — those
-    // are compacted and sorted in registers, not the whole list
+    // registers: the sample key at the rank where ~2 k keys are expected at or
+    // above it); when k to 512 keys reach t1 — they hold the top k — those
+    // are compacted and sorted in registers, not the whole list.  (The kernel
+    // waits for its slowest query; a debug build counted no miss of this
+    // window over a W = 8 batch.)
     uint64_t smp[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) smp[j] = kb[(((uint32_t)j * 64u + lane) * cnt) >> 7];
     wave_sort_regs<2>(smp);
-    const int r = min(127, max(0, (int)((3u * (uint32_t)k * 64u) / cnt)));
+    const int r = min(127, max(0, (int)((4u * (uint32_t)k * 64u) / cnt)));
     const uint64_t t1 = __shfl(r >= 64 ? smp[1] : smp[0], r & 63, 64);
     uint64_t key[kMergeSortedCap / 64];
     uint32_t c = 0u;
@@ -3426,7 +3431,7 @@ __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
       c += key[j] != 0ull && key[j] >= t1;
     }
     c = wave_sum_u32(c);
-    if (t1 != 0ull && c >= (uint32_t)k && c <= 256u) {
+    if (t1 != 0ull && c >= (uint32_t)k && c <= 512u) {
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       uint32_t base = 0u;
 #pragma unroll
@@ -3439,10 +3444,14 @@ __global__ __launch_bounds__(64 * kQW) void merge_sorted_kernel(
         base += (uint32_t)__popcll(b);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      regs_sort_write<4>(kb, base, k, 0, q, docs, scores);
+      if (base <= 256u)
+        regs_sort_write<4>(kb, base, k, 0, q, docs, scores);
+      else
+        regs_sort_write<8>(kb, base, k, 0, q, docs, scores);
       return;
     }
   }
+
   if (cnt <= 512u) {
     sort_write_any<8>(kb, cnt, k, 0, q, docs, scores);
     return;

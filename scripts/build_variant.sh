@@ -7,10 +7,11 @@ set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
 OBJ=$R/mojo-bm25_amd/bm25mi/_obj
-mkdir -p $R/exp
+OUTD=${OUTD:-$R/exp}
+mkdir -p $OUTD
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Wno-unused-value \
-  "$@" -c -o $R/exp/k_$NAME.o $R/mojo-bm25_amd/csrc/bm25mi_kernels.hip
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/exp/libbm25mi_$NAME.so \
-  $R/exp/k_$NAME.o $OBJ/bm25mi_large.o $OBJ/bm25mi_build.o $OBJ/bm25mi_sort.o $OBJ/bm25mi_dense.o $OBJ/bm25mi_capi.o
-rm -f $R/exp/k_$NAME.o
-echo $R/exp/libbm25mi_$NAME.so
+  "$@" -c -o $OUTD/k_$NAME.o $R/mojo-bm25_amd/csrc/bm25mi_kernels.hip
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUTD/libbm25mi_$NAME.so \
+  $OUTD/k_$NAME.o $OBJ/bm25mi_large.o $OBJ/bm25mi_build.o $OBJ/bm25mi_sort.o $OBJ/bm25mi_dense.o $OBJ/bm25mi_capi.o
+rm -f $OUTD/k_$NAME.o
+echo $OUTD/libbm25mi_$NAME.so
