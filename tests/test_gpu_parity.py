@@ -1316,6 +1316,42 @@ def test_rccl_all_gather_branch(gpu):
         dist.destroy_process_group()
 
 
+def test_rccl_one_collective_protocol_one_rank(gpu):
+    """The one-collective protocol end to end over a real one-rank RCCL
+    communicator (the driver's N > 1 bench path, minus the peers):
+    setup_world_bounds' MAX / SUM all-reduces and the int32-view all-gather
+    of the bounds on RCCL, the pooled world table, bm25_search_shard_device
+    and the W-way merge of sharded_search (its list all-gather is the
+    identity at one rank: test_rccl_all_gather_branch covers it) —
+    bit-exact against the oracle; a second search reuses the setup."""
+    import torch
+    import torch.distributed as dist
+    from bm25mi.dist import setup_world_bounds, sharded_search
+    N, V = 1_200_000, 300
+    ip, ix, dt = _bound_case(95, N, V, 30)
+    rng = np.random.default_rng(12)
+    q = np.concatenate([rng.integers(0, 30, size=(64, 4)),
+                        rng.integers(30, V, size=(64, 4))], axis=1).astype(np.int32)
+    k = 10
+    ref = oracle.search_c(N, ip, ix, dt, q, k, threads=8)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        index = _idx(ip, ix, dt, N, segments="dense")
+        assert setup_world_bounds(index)
+        dq = torch.from_numpy(q).cuda()
+        d = torch.empty((len(q), k), dtype=torch.int32, device="cuda")
+        sc = torch.empty((len(q), k), dtype=torch.float32, device="cuda")
+        for _ in range(2):
+            docs, scores = sharded_search(index, dq, k, N, d, sc)
+            torch.cuda.synchronize()
+            _exact((docs.cpu().numpy(), scores.cpu().numpy()), ref)
+            assert {"bound_keys", "bound_pool"} <= index.last_dispatch()["kernels"]
+        index.close()
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("T", [4, 8])
 def test_tile_bound_skips_exact(gpu, T):
     """The REST pass skips the (query, tile) pairs whose query-term maxima
