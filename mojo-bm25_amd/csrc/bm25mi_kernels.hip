@@ -2718,6 +2718,12 @@ __device__ __forceinline__ void sort_write_any(uint64_t* keys, uint32_t n, int32
 }
 
 constexpr int kFastR = 32;      // list keys per lane held in registers
+// lists longer than this at k <= 128 go to merge_tail_kernel's block merge
+// (block_long_merge: 1024 threads load them in one round)
+#ifndef BM25_BLOCK_LONG
+#define BM25_BLOCK_LONG 512
+#endif
+constexpr int kBlockLongMin = BM25_BLOCK_LONG;
 constexpr int kFastMaxK = 1024; // largest k served (LDS: k keys per wave)
 
 __device__ __forceinline__ void wave_sort_write(uint64_t* keys, uint32_t n, int m, int32_t k,
@@ -3121,11 +3127,15 @@ __global__ __launch_bounds__(64 * kQW) void merge_fast_kernel(Stage sg, int32_t 
     }
     return;
   }
-  // a list of more than 1024 keys at k <= 128 (a few queries whose threshold
-  // sits far below their k-th key): merge_tail_kernel's block merge, whose
-  // 1024 threads load it in one round (block_long_merge); one wave alone
-  // kept the whole merge waiting ~20 us for such a query
-  const bool block_long = cnt > 1024 && k <= 128 && th != kZeroFillTheta;
+  // a list of more than kBlockLongMin = 512 keys at k <= 128 (a few queries
+  // whose threshold sits far below their k-th key): merge_tail_kernel's block
+  // merge, whose 1024 threads load it in one round (block_long_merge); one
+  // wave alone kept the whole merge waiting ~20 us for such a query (config
+  // 3: merge_fast 15.5 -> 11.2 us with 512 in place of 1024, the tail alike)
+  // (a doc shard's unsorted list of <= 1024 keys stays here: its best k are
+  // selected in registers, no sort — faster than the block merge's sorts)
+  const bool block_long = (cnt > 1024 || (cnt > kBlockLongMin && !sg.unsorted)) && k <= 128 &&
+                          th != kZeroFillTheta;
   if (!block_long && cnt > 64 * kFastR &&
       long_merge_one(sg, k, doc_offset, q, cnt, keys, hist[threadIdx.x >> 6], docs, scores))
     return;
@@ -3193,7 +3203,7 @@ __device__ bool block_long_merge(const Stage& sg, int32_t k, int64_t doc_offset,
                                  int32_t* __restrict__ docs, float* __restrict__ scores) {
   const int32_t cnt = sg.list_cnt[q];
   const uint64_t th = sg.theta[q];
-  if (cnt <= 1024 || cnt > kMergeP || k > 128 || th == kZeroFillTheta) return false;
+  if (cnt <= kBlockLongMin || cnt > kMergeP || k > 128 || th == kZeroFillTheta) return false;
   const uint64_t* lst = sg.list + q * (int64_t)sg.C;
   const uint32_t lane = lane_id();
   uint64_t x[kLongPT];
